@@ -1,0 +1,74 @@
+// ffcv_common.hip -- error state, device/stream/memory helpers and the
+// reference-compatible my_memcpy (libffcv.cpp:44-46).
+#include <cstring>
+#include <string>
+
+#include "api_internal.h"
+
+namespace ffcv {
+static thread_local std::string g_last_error;
+
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+int check_hip(hipError_t e, const char *what) {
+  set_error("%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+  return e == hipErrorOutOfMemory ? FFCV_ENOMEM : FFCV_EHIP;
+}
+}  // namespace ffcv
+
+extern "C" {
+
+int ffcv_abi_version(void) { return FFCV_HIP_ABI_VERSION; }
+
+const char *ffcv_last_error(void) { return ffcv::g_last_error.c_str(); }
+
+int ffcv_device_count(int *count) {
+  if (!count) {
+    ffcv::set_error("ffcv_device_count: count is NULL");
+    return FFCV_EINVAL;
+  }
+  FFCV_HIP_CHECK(hipGetDeviceCount(count));
+  return FFCV_OK;
+}
+
+int ffcv_set_device(int device) {
+  FFCV_HIP_CHECK(hipSetDevice(device));
+  return FFCV_OK;
+}
+
+int ffcv_stream_synchronize(void *stream) {
+  FFCV_HIP_CHECK(hipStreamSynchronize(ffcv::as_stream(stream)));
+  return FFCV_OK;
+}
+
+int ffcv_malloc(void **dptr, uint64_t bytes) {
+  FFCV_HIP_CHECK(hipMalloc(dptr, bytes));
+  return FFCV_OK;
+}
+
+int ffcv_free(void *dptr) {
+  FFCV_HIP_CHECK(hipFree(dptr));
+  return FFCV_OK;
+}
+
+int ffcv_memcpy_h2d_async(void *dst, const void *src, uint64_t bytes, void *stream) {
+  FFCV_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ffcv::as_stream(stream)));
+  return FFCV_OK;
+}
+
+int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stream) {
+  FFCV_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ffcv::as_stream(stream)));
+  return FFCV_OK;
+}
+
+// libffcv.cpp:44-46: my_memcpy(source, dst, size) -- host plumbing only.
+void my_memcpy(void *source, void *dst, uint64_t size) { std::memcpy(dst, source, size); }
+
+}  // extern "C"

@@ -1,0 +1,328 @@
+// ffcv_rrc.hip -- device random draws, raw-mode crop+INTER_AREA resize with a
+// fused flip / cutout / LUT-normalize epilogue, and the standalone transforms.
+//
+// Reference path (raw mode): rgb_image.py:202-208 takes a
+// zero-copy view of the mmap'd sample, get_random_crop draws the window and
+// libffcv.cpp:33-42 cv::resize(INTER_AREA) writes the output; Cutout
+// (cutout.py:36-47) and NormalizeImage (normalize.py:65) follow as separate
+// passes.  Here the .beton bytes are already resident in HBM, so one launch
+// reads each crop ROI once and writes the final (u8 or fp16) pixels once.
+#include "api_internal.h"
+#include "device_common.h"
+
+// ------------------------------------------------------------ draws -------
+__global__ void __launch_bounds__(64) draw_kernel(const uint64_t *__restrict__ ids,
+                                                  const ffcv_sample *__restrict__ samples, int B,
+                                                  ffcv_draw_params p, int32_t *__restrict__ crops,
+                                                  int32_t *__restrict__ cut, uint8_t *__restrict__ flips,
+                                                  int32_t *__restrict__ status) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B) return;
+  uint64_t id = ids[k];
+  uint32_t H = samples[k].height, W = samples[k].width;
+  int err = 0;
+  DevMT m;
+  if (crops) {
+    int32_t c[4];
+    if (p.crop_kind == 0) {
+      mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 1));
+      random_crop(m, H, W, p.scale, p.ratio, c);
+      err |= m.err;
+    } else {
+      center_crop(H, W, p.center_ratio, c);
+    }
+    crops[4 * k + 0] = c[0];
+    crops[4 * k + 1] = c[1];
+    crops[4 * k + 2] = c[2];
+    crops[4 * k + 3] = c[3];
+  }
+  if (cut && p.cutout_size > 0) {
+    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 2));
+    cut[2 * k + 0] = (int32_t)mt_randint(m, p.out_h - p.cutout_size + 1);
+    cut[2 * k + 1] = (int32_t)mt_randint(m, p.out_w - p.cutout_size + 1);
+    err |= m.err;
+  }
+  if (flips) {
+    // flip.py:35 rand() < flip_prob, one draw per sample under the contract
+    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 3));
+    double u = mt_double(m);
+    flips[k] = (uint8_t)(u < (double)p.flip_prob_x1e6 * 1e-6);
+  }
+  if (status) status[k] = err ? FFCV_SAMPLE_RNG : FFCV_SAMPLE_OK;
+}
+
+// ------------------------------------------------ raw crop + resize -------
+struct GlobalSrc {
+  const uint8_t *p;
+  uint64_t step;
+  FFCV_DEV int at(int y, int x, int c) const { return p[(uint64_t)y * step + (uint64_t)x * 3 + c]; }
+};
+
+template <bool FP16>
+FFCV_DEV void store_px(void *out, uint64_t idx, const int v[3], const uint16_t *lut) {
+  if (FP16) {
+    uint16_t *o = (uint16_t *)out + idx * 3;
+    o[0] = lut[v[0] * 3 + 0];
+    o[1] = lut[v[1] * 3 + 1];
+    o[2] = lut[v[2] * 3 + 2];
+  } else {
+    uint8_t *o = (uint8_t *)out + idx * 3;
+    o[0] = (uint8_t)v[0];
+    o[1] = (uint8_t)v[1];
+    o[2] = (uint8_t)v[2];
+  }
+}
+
+#define RRC_THREADS 256
+#define RRC_PPT 4
+
+template <bool FP16>
+__global__ void __launch_bounds__(RRC_THREADS)
+    rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
+                   const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
+                   const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
+                   void *__restrict__ out) {
+  __shared__ uint16_t s_lut[FP16 ? 768 : 1];
+  const int k = blockIdx.y;
+  const ffcv_sample s = samples[k];
+  if (FP16) {
+    for (int i = threadIdx.x; i < 768; i += RRC_THREADS) s_lut[i] = p.lut[i];
+    __syncthreads();
+  }
+  if (s.mode != 1) return;
+  const int ci = crops[4 * k], cj = crops[4 * k + 1], chh = crops[4 * k + 2], cww = crops[4 * k + 3];
+  GlobalSrc src{base + s.offset + ((uint64_t)ci * s.width + cj) * 3, (uint64_t)s.width * 3};
+  ResizePlan P = make_plan(cww, chh, p.out_w, p.out_h);
+  Epilogue ep;
+  ep.out_h = p.out_h;
+  ep.out_w = p.out_w;
+  ep.cut_size = cut ? p.cutout_size : 0;
+  ep.cut_y = cut ? cut[2 * k] : 0;
+  ep.cut_x = cut ? cut[2 * k + 1] : 0;
+  ep.flip = flips ? flips[k] : 0;
+  ep.cut_before_flip = p.cutout_fill[3];
+  ep.fill[0] = p.cutout_fill[0];
+  ep.fill[1] = p.cutout_fill[1];
+  ep.fill[2] = p.cutout_fill[2];
+  const int npx = p.out_h * p.out_w;
+  char *o = (char *)out + stride * k;
+  const int first = blockIdx.x * RRC_THREADS * RRC_PPT + threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < RRC_PPT; r++) {
+    int px = first + r * RRC_THREADS;
+    if (px >= npx) break;
+    int dy = px / p.out_w, dx = px - dy * p.out_w;
+    int v[3];
+    if (ep.in_cut(dy, dx)) {
+      v[0] = ep.fill[0];
+      v[1] = ep.fill[1];
+      v[2] = ep.fill[2];
+    } else {
+      resize_pixel(P, src, dy, ep.src_x(dx), v);
+    }
+    store_px<FP16>(o, px, v, s_lut);
+  }
+}
+
+// --------------------------------------------- simple (raw) gather -------
+__global__ void __launch_bounds__(256) gather_raw_kernel(const uint8_t *__restrict__ base,
+                                                         const ffcv_sample *__restrict__ samples,
+                                                         uint8_t *__restrict__ out, uint64_t stride) {
+  const int k = blockIdx.y;
+  const ffcv_sample s = samples[k];
+  if (s.mode != 1) return;
+  const uint8_t *src = base + s.offset;
+  uint8_t *dst = out + stride * k;
+  uint64_t n = s.size;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) gather_samples_kernel(const ffcv_sample *__restrict__ table, uint64_t n,
+                                                             const uint64_t *__restrict__ ids, int B,
+                                                             ffcv_sample *__restrict__ out) {
+  int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= B) return;
+  uint64_t i = ids[k];
+  ffcv_sample s;
+  if (i < n) {
+    s = table[i];
+  } else {  // out-of-range index: an empty jpg sample -> BAD_MARKER status
+    s.offset = 0;
+    s.size = 0;
+    s.height = s.width = 1;
+    s.mode = 0;
+    s.reserved = 0;
+  }
+  out[k] = s;
+}
+
+// ------------------------------------------------------ standalone -------
+__global__ void __launch_bounds__(256) cutout_kernel(uint8_t *__restrict__ img, int H, int W,
+                                                     const int32_t *__restrict__ yx, int c, uint8_t f0,
+                                                     uint8_t f1, uint8_t f2) {
+  const int k = blockIdx.x;
+  const int y0 = yx[2 * k], x0 = yx[2 * k + 1];
+  uint8_t *base = img + (uint64_t)k * H * W * 3;
+  for (int i = threadIdx.x; i < c * c; i += 256) {
+    int y = y0 + i / c, x = x0 + i % c;
+    if (y < H && x < W) {
+      uint8_t *p = base + ((uint64_t)y * W + x) * 3;
+      p[0] = f0;
+      p[1] = f1;
+      p[2] = f2;
+    }
+  }
+}
+
+// normalize.py:65: output = table[input * 3 + i % 3]; 12 elements (4 RGB
+// pixels) per lane so loads/stores are dword-shaped.
+__global__ void __launch_bounds__(256) normalize_kernel(const uint8_t *__restrict__ in, uint64_t n,
+                                                        const uint16_t *__restrict__ lut,
+                                                        uint16_t *__restrict__ out) {
+  __shared__ uint16_t s_lut[768];
+  for (int i = threadIdx.x; i < 768; i += 256) s_lut[i] = lut[i];
+  __syncthreads();
+  uint64_t groups = n / 12;
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * 256) {
+    const uint8_t *ip = in + g * 12;
+    uint16_t *op = out + g * 12;
+#pragma unroll
+    for (int e = 0; e < 12; e++) op[e] = s_lut[ip[e] * 3 + (e % 3)];
+  }
+  if (blockIdx.x == 0) {
+    for (uint64_t i = groups * 12 + threadIdx.x; i < n; i += 256) out[i] = s_lut[in[i] * 3 + (i % 3)];
+  }
+}
+
+__global__ void __launch_bounds__(256) flip_kernel(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                   int H, int W, int cb, const uint8_t *__restrict__ flips) {
+  const int k = blockIdx.y;
+  const uint64_t img = (uint64_t)H * W * cb;
+  const bool f = flips[k] != 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < img; i += (uint64_t)gridDim.x * 256) {
+    uint64_t px = i / cb;
+    int b = (int)(i - px * cb);
+    int y = (int)(px / W), x = (int)(px - (uint64_t)y * W);
+    int sx = f ? W - 1 - x : x;
+    out[k * img + i] = in[k * img + ((uint64_t)y * W + sx) * cb + b];
+  }
+}
+
+// ---------------------------------------------------------- C ABI -------
+extern "C" {
+
+int ffcv_draw_batch(void *stream, const uint64_t *sample_ids, const ffcv_sample *samples, int batch,
+                    const ffcv_draw_params *p, int32_t *crops, int32_t *cutout_yx, uint8_t *flips,
+                    int32_t *status) {
+  if (batch < 0 || !p || !sample_ids || !samples) {
+    ffcv::set_error("ffcv_draw_batch: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  if (p->cutout_size > 0 && (p->cutout_size > p->out_h || p->cutout_size > p->out_w)) {
+    ffcv::set_error("ffcv_draw_batch: cutout_size %d exceeds output %dx%d", p->cutout_size, p->out_h,
+                    p->out_w);
+    return FFCV_EINVAL;
+  }
+  hipLaunchKernelGGL(draw_kernel, dim3((batch + 63) / 64), dim3(64), 0, ffcv::as_stream(stream),
+                     sample_ids, samples, batch, *p, crops, cutout_yx, flips, status);
+  FFCV_LAUNCH_CHECK("draw_kernel");
+  return FFCV_OK;
+}
+
+int ffcv_rrc_raw_batch(void *stream, const uint8_t *base, const ffcv_sample *samples, int batch,
+                       const int32_t *crops, const int32_t *cutout_yx, const uint8_t *flips,
+                       const ffcv_rrc_params *p, void *out) {
+  if (batch < 0 || !p || !base || !samples || !crops || !out || p->out_h <= 0 || p->out_w <= 0) {
+    ffcv::set_error("ffcv_rrc_raw_batch: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  const bool fp16 = p->lut != nullptr;
+  uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
+  uint64_t stride = p->out_stride ? p->out_stride : dense;
+  int npx = p->out_h * p->out_w;
+  dim3 grid((npx + RRC_THREADS * RRC_PPT - 1) / (RRC_THREADS * RRC_PPT), batch);
+  if (fp16)
+    hipLaunchKernelGGL(rrc_raw_kernel<true>, grid, dim3(RRC_THREADS), 0, ffcv::as_stream(stream), base,
+                       samples, crops, cutout_yx, flips, *p, stride, out);
+  else
+    hipLaunchKernelGGL(rrc_raw_kernel<false>, grid, dim3(RRC_THREADS), 0, ffcv::as_stream(stream), base,
+                       samples, crops, cutout_yx, flips, *p, stride, out);
+  FFCV_LAUNCH_CHECK("rrc_raw_kernel");
+  return FFCV_OK;
+}
+
+int ffcv_gather_samples(void *stream, const ffcv_sample *table, uint64_t n_table, const uint64_t *ids,
+                        int batch, ffcv_sample *out) {
+  if (!table || !ids || !out || batch < 0) {
+    ffcv::set_error("ffcv_gather_samples: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  hipLaunchKernelGGL(gather_samples_kernel, dim3((batch + 255) / 256), dim3(256), 0, ffcv::as_stream(stream),
+                     table, n_table, ids, batch, out);
+  FFCV_LAUNCH_CHECK("gather_samples_kernel");
+  return FFCV_OK;
+}
+
+int ffcv_gather_raw_batch(void *stream, const uint8_t *base, const ffcv_sample *samples, int batch,
+                          uint8_t *out, uint64_t out_stride) {
+  if (batch < 0 || !base || !samples || !out || !out_stride) {
+    ffcv::set_error("ffcv_gather_raw_batch: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  unsigned gx = (unsigned)((out_stride + 255) / 256);
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(gather_raw_kernel, dim3(gx, batch), dim3(256), 0, ffcv::as_stream(stream), base,
+                     samples, out, out_stride);
+  FFCV_LAUNCH_CHECK("gather_raw_kernel");
+  return FFCV_OK;
+}
+
+int ffcv_cutout_batch(void *stream, uint8_t *images, int batch, int height, int width,
+                      const int32_t *cutout_yx, int crop_size, const uint8_t fill[3]) {
+  if (batch < 0 || !images || !cutout_yx || crop_size <= 0 || crop_size > height || crop_size > width) {
+    ffcv::set_error("ffcv_cutout_batch: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  hipLaunchKernelGGL(cutout_kernel, dim3(batch), dim3(256), 0, ffcv::as_stream(stream), images, height,
+                     width, cutout_yx, crop_size, fill[0], fill[1], fill[2]);
+  FFCV_LAUNCH_CHECK("cutout_kernel");
+  return FFCV_OK;
+}
+
+int ffcv_normalize_batch(void *stream, const uint8_t *in, uint64_t n, const uint16_t *lut, uint16_t *out) {
+  if (!in || !lut || !out) {
+    ffcv::set_error("ffcv_normalize_batch: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (n == 0) return FFCV_OK;
+  uint64_t groups = n / 12 + 1;
+  unsigned gx = (unsigned)((groups + 255) / 256);
+  if (gx > 4096) gx = 4096;
+  hipLaunchKernelGGL(normalize_kernel, dim3(gx), dim3(256), 0, ffcv::as_stream(stream), in, n, lut, out);
+  FFCV_LAUNCH_CHECK("normalize_kernel");
+  return FFCV_OK;
+}
+
+int ffcv_flip_batch(void *stream, const uint8_t *in, uint8_t *out, int batch, int height, int width,
+                    int channels_bytes, const uint8_t *flips) {
+  if (batch < 0 || !in || !out || !flips || in == out || height <= 0 || width <= 0 || channels_bytes <= 0) {
+    ffcv::set_error("ffcv_flip_batch: invalid arguments (in-place flip unsupported)");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  uint64_t img = (uint64_t)height * width * channels_bytes;
+  unsigned gx = (unsigned)((img + 255) / 256);
+  if (gx > 256) gx = 256;
+  hipLaunchKernelGGL(flip_kernel, dim3(gx, batch), dim3(256), 0, ffcv::as_stream(stream), in, out, height,
+                     width, channels_bytes, flips);
+  FFCV_LAUNCH_CHECK("flip_kernel");
+  return FFCV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,241 @@
+"""ctypes binding of ``libffcv_hip.so`` (include/ffcv_hip.h).
+
+Replaces the reference's ``ffcv/libffcv.py`` (CDLL of ``ffcv._libffcv``,
+ffcv/libffcv.py:8-55).  The reference binds one-sample CPU functions
+(``resize``, ``imdecode``, ``my_memcpy``) called from numba ``prange``
+workers.  This binding exposes the batch/device ABI: every call enqueues HIP
+work on the caller's stream (``torch.cuda.current_stream().cuda_stream`` is a
+``hipStream_t`` on ROCm) and takes device pointers (``tensor.data_ptr()``).
+
+The library is built in-tree (``python -m ffcv_amd._build``).  There is no CPU
+fallback for any compute entry point: if the shared object is missing this
+module raises at import of the compute functions.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libffcv_hip.so')
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int32 = ctypes.c_int32
+c_uint32 = ctypes.c_uint32
+c_uint64 = ctypes.c_uint64
+
+# per-sample device status codes (FFCV_SAMPLE_*)
+SAMPLE_STATUS = {0: 'ok', 1: 'bad marker', 2: 'unsupported JPEG feature',
+                 3: 'image larger than decoder context', 4: 'corrupt entropy stream',
+                 5: 'geometry mismatch', 6: 'rng stream exhausted'}
+
+
+class FFCVError(RuntimeError):
+    pass
+
+
+class Sample(ctypes.Structure):
+    """ffcv_sample (32 bytes)."""
+    _fields_ = [('offset', c_uint64), ('size', c_uint64), ('height', c_uint32),
+                ('width', c_uint32), ('mode', c_uint32), ('reserved', c_uint32)]
+
+
+SAMPLE_DTYPE = np.dtype([('offset', '<u8'), ('size', '<u8'), ('height', '<u4'),
+                         ('width', '<u4'), ('mode', '<u4'), ('reserved', '<u4')])
+assert SAMPLE_DTYPE.itemsize == ctypes.sizeof(Sample) == 32
+
+
+class RRCParams(ctypes.Structure):
+    _fields_ = [('out_h', c_int32), ('out_w', c_int32), ('cutout_size', c_int32),
+                ('cutout_fill', ctypes.c_uint8 * 4), ('lut', c_void_p),
+                ('out_stride', c_uint64)]
+
+
+class DrawParams(ctypes.Structure):
+    _fields_ = [('crop_kind', c_int32), ('out_h', c_int32), ('out_w', c_int32),
+                ('cutout_size', c_int32), ('scale', ctypes.c_double * 2),
+                ('ratio', ctypes.c_double * 2), ('center_ratio', ctypes.c_double),
+                ('loader_seed', c_uint64), ('epoch', c_uint64),
+                ('flip_prob_x1e6', c_int32), ('reserved', c_int32)]
+
+
+_lib = None
+
+_SIGS = {
+    'ffcv_abi_version': (c_int, []),
+    'ffcv_last_error': (ctypes.c_char_p, []),
+    'ffcv_device_count': (c_int, [c_void_p]),
+    'ffcv_set_device': (c_int, [c_int]),
+    'ffcv_stream_synchronize': (c_int, [c_void_p]),
+    'ffcv_malloc': (c_int, [c_void_p, c_uint64]),
+    'ffcv_free': (c_int, [c_void_p]),
+    'ffcv_memcpy_h2d_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    'ffcv_memcpy_d2h_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    'my_memcpy': (None, [c_void_p, c_void_p, c_uint64]),
+    'ffcv_draw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p]),
+    'ffcv_rrc_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p]),
+    'ffcv_gather_samples': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_int, c_void_p]),
+    'ffcv_gather_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_uint64]),
+    'ffcv_jpeg_create': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64]),
+    'ffcv_jpeg_destroy': (c_int, [c_void_p]),
+    'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'ffcv_jpeg_decode_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_uint64, c_void_p]),
+    'ffcv_jpeg_coefficients_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                             c_void_p, c_uint64, c_void_p]),
+    'ffcv_cutout_batch': (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                  c_void_p]),
+    'ffcv_normalize_batch': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+    'ffcv_flip_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                c_void_p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def lib():
+    """Load libffcv_hip.so (raises if it was not built -- no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FFCVError(f'{LIB_PATH} is missing: build it with `python -m ffcv_amd._build` '
+                            '(there is no CPU fallback for the decode path)')
+        # Load torch's HIP runtime first: libffcv_hip.so's NEEDED
+        # libamdhip64.so.7 then binds to the runtime torch already uses
+        # (same soname), so tensors and our kernels share one HIP runtime.
+        # Loading ours first would pull /opt/rocm's copy and give the process
+        # two runtimes ("no ROCm-capable device" in the second).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        if l.ffcv_abi_version() != 1:
+            raise FFCVError('libffcv_hip.so ABI version mismatch')
+        _lib = l
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = lib().ffcv_last_error().decode(errors='replace')
+        raise FFCVError(f'{what} failed ({rc}): {msg}')
+
+
+def _p(x):
+    """Device/host pointer of a torch tensor, numpy array, int or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return c_void_p(x)
+    if hasattr(x, 'data_ptr'):
+        return c_void_p(x.data_ptr())
+    if isinstance(x, np.ndarray):
+        return c_void_p(x.ctypes.data)
+    raise TypeError(type(x))
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return c_void_p(stream.cuda_stream if hasattr(stream, 'cuda_stream') else int(stream))
+
+
+# ----------------------------------------------------------------- wrappers
+def memcpy(source: np.ndarray, dest: np.ndarray):
+    """ffcv/libffcv.py:51-55 memcpy (host plumbing)."""
+    lib().my_memcpy(source.ctypes.data, dest.ctypes.data, source.size * source.itemsize)
+
+
+def draw_batch(ids, samples, params: DrawParams, crops=None, cutout_yx=None, flips=None,
+               status=None, stream=None):
+    _check(lib().ffcv_draw_batch(_stream(stream), _p(ids), _p(samples), int(ids.shape[0]),
+                                 ctypes.byref(params), _p(crops), _p(cutout_yx), _p(flips),
+                                 _p(status)), 'ffcv_draw_batch')
+
+
+def gather_samples(table, ids, out, stream=None):
+    _check(lib().ffcv_gather_samples(_stream(stream), _p(table), int(table.shape[0]), _p(ids),
+                                     int(ids.shape[0]), _p(out)), 'ffcv_gather_samples')
+
+
+def rrc_raw_batch(base, samples, batch, crops, cutout_yx, flips, params: RRCParams, out,
+                  stream=None):
+    _check(lib().ffcv_rrc_raw_batch(_stream(stream), _p(base), _p(samples), int(batch),
+                                    _p(crops), _p(cutout_yx), _p(flips), ctypes.byref(params),
+                                    _p(out)), 'ffcv_rrc_raw_batch')
+
+
+def gather_raw_batch(base, samples, batch, out, out_stride, stream=None):
+    _check(lib().ffcv_gather_raw_batch(_stream(stream), _p(base), _p(samples), int(batch),
+                                       _p(out), int(out_stride)), 'ffcv_gather_raw_batch')
+
+
+def cutout_batch(images, yx, crop_size, fill, stream=None):
+    B, H, W = int(images.shape[0]), int(images.shape[1]), int(images.shape[2])
+    f = (ctypes.c_uint8 * 3)(*[int(x) for x in fill])
+    _check(lib().ffcv_cutout_batch(_stream(stream), _p(images), B, H, W, _p(yx), int(crop_size),
+                                   f), 'ffcv_cutout_batch')
+
+
+def normalize_batch(inp, lut, out, stream=None):
+    _check(lib().ffcv_normalize_batch(_stream(stream), _p(inp), int(inp.numel()), _p(lut),
+                                      _p(out)), 'ffcv_normalize_batch')
+
+
+def flip_batch(inp, out, flips, stream=None):
+    B, H, W = int(inp.shape[0]), int(inp.shape[1]), int(inp.shape[2])
+    cb = int(inp[0, 0, 0].numel() * inp.element_size())
+    _check(lib().ffcv_flip_batch(_stream(stream), _p(inp), _p(out), B, H, W, cb, _p(flips)),
+           'ffcv_flip_batch')
+
+
+class JpegDecoder:
+    """Owns an ffcv_jpeg_ctx (scratch for max_batch images)."""
+
+    def __init__(self, max_batch, max_height, max_width, max_bytes):
+        self.handle = c_void_p()
+        self.max_batch = int(max_batch)
+        self.max_height, self.max_width = int(max_height), int(max_width)
+        self.max_bytes = int(max_bytes)
+        _check(lib().ffcv_jpeg_create(ctypes.byref(self.handle), self.max_batch,
+                                      self.max_height, self.max_width, self.max_bytes),
+               'ffcv_jpeg_create')
+
+    def rrc(self, base, samples, batch, crops, cutout_yx, flips, params: RRCParams, out,
+            status, stream=None):
+        _check(lib().ffcv_jpeg_rrc_batch(self.handle, _stream(stream), _p(base), _p(samples),
+                                         int(batch), _p(crops), _p(cutout_yx), _p(flips),
+                                         ctypes.byref(params), _p(out), _p(status)),
+               'ffcv_jpeg_rrc_batch')
+
+    def decode(self, base, samples, batch, out, out_stride, status, stream=None):
+        _check(lib().ffcv_jpeg_decode_batch(self.handle, _stream(stream), _p(base), _p(samples),
+                                            int(batch), _p(out), int(out_stride), _p(status)),
+               'ffcv_jpeg_decode_batch')
+
+    def coefficients(self, base, samples, batch, out, max_blocks, status, stream=None):
+        _check(lib().ffcv_jpeg_coefficients_batch(self.handle, _stream(stream), _p(base),
+                                                  _p(samples), int(batch), _p(out),
+                                                  int(max_blocks), _p(status)),
+               'ffcv_jpeg_coefficients_batch')
+
+    def close(self):
+        if self.handle:
+            lib().ffcv_jpeg_destroy(self.handle)
+            self.handle = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

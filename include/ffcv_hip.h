@@ -1,0 +1,208 @@
+/*
+ * ffcv_hip.h -- C ABI of libffcv_hip.so, the MI355X (gfx950) replacement for
+ * the reference's native shim.
+ *
+ * Reference boundary being replaced:
+ *   /root/reference/libffcv/libffcv.cpp   (exports resize / my_memcpy /
+ *                                          my_fread / imdecode, :33-112)
+ *   /root/reference/ffcv/libffcv.py       (ctypes binding, :8-55)
+ * The reference binds ONE sample per call from numba prange workers.  This
+ * ABI is batch- and device-first: every compute entry point takes a device
+ * base pointer to the .beton bytes resident in HBM, a device array of
+ * per-sample descriptors, and a hipStream_t (passed as void*) on which all
+ * work is enqueued asynchronously.  No torch types, no hidden hipMalloc in a
+ * launch, no host synchronisation in a launch (graph-capturable).
+ *
+ * Ownership: the caller owns every input/output buffer.  The library owns
+ * only the scratch inside an ffcv_jpeg_ctx (allocated once at create time).
+ *
+ * Errors: every function returns an int status (FFCV_OK == 0).  On failure a
+ * thread-local message is available from ffcv_last_error().  Per-sample
+ * decode failures (corrupt / unsupported JPEG) are reported in a device
+ * int32 status array and the sample's output is zero-filled; the reference
+ * ignores imdecode's return code (rgb_image.py:131,196) and yields garbage.
+ */
+#ifndef FFCV_HIP_H
+#define FFCV_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFCV_HIP_ABI_VERSION 1
+
+enum {
+  FFCV_OK = 0,
+  FFCV_EINVAL = -1,      /* bad argument */
+  FFCV_EHIP = -2,        /* HIP runtime error */
+  FFCV_ENOMEM = -3,      /* allocation failed */
+  FFCV_EUNSUPPORTED = -4 /* feature not on this path */
+};
+
+/* Per-sample status codes written by the device (int32). */
+enum {
+  FFCV_SAMPLE_OK = 0,
+  FFCV_SAMPLE_BAD_MARKER = 1,      /* not a JPEG / truncated header */
+  FFCV_SAMPLE_UNSUPPORTED = 2,     /* progressive, arithmetic, 12-bit, DRI, CMYK */
+  FFCV_SAMPLE_TOO_LARGE = 3,       /* exceeds the ctx's max_height/max_width */
+  FFCV_SAMPLE_CORRUPT = 4,         /* entropy stream inconsistent */
+  FFCV_SAMPLE_GEOMETRY = 5,        /* SOF size != .beton metadata */
+  FFCV_SAMPLE_RNG = 6              /* > 623 MT19937 draws for one stream */
+};
+
+/* One sample of a batch, as resolved from the .beton metadata + allocation
+ * table (rgb_image.py:302-308 metadata; memory_managers/os_cache.py:55-60
+ * read).  32 bytes, device-resident array. */
+typedef struct ffcv_sample {
+  uint64_t offset; /* byte offset of the sample's data from the base pointer */
+  uint64_t size;   /* byte count (allocation table 'size') */
+  uint32_t height; /* metadata 'height' */
+  uint32_t width;  /* metadata 'width' */
+  uint32_t mode;   /* 0 = jpg, 1 = raw (rgb_image.py:21-23) */
+  uint32_t reserved;
+} ffcv_sample;
+
+/* Parameters of a fused decode -> crop -> resize -> cutout -> normalize
+ * launch (rgb_image.py:168-212, cutout.py:31-52, normalize.py:58-87). */
+typedef struct ffcv_rrc_params {
+  int32_t out_h, out_w;    /* output_size (rgb_image.py:145-149) */
+  int32_t cutout_size;     /* 0: no cutout; else crop_size (cutout.py:26) */
+  uint8_t cutout_fill[4];  /* fill RGB (cutout.py:29); [3] = 1 when the
+                              pipeline runs Cutout BEFORE RandomHorizontalFlip
+                              (0: flip first, then cutout) */
+  const uint16_t *lut;     /* device [256][3] fp16 bits (normalize.py:42-49), or
+                              NULL for uint8 output */
+  uint64_t out_stride;     /* bytes between samples in the output; 0 = dense */
+} ffcv_rrc_params;
+
+/* Crop-draw parameters (rgb_image.py:48-81) + seeding contract
+ * (DESIGN.md "RNG contract": one MT19937 per (op, sample, epoch) seeded
+ * with low32(splitmix64 chain of loader_seed, epoch, sample index, op id)). */
+typedef struct ffcv_draw_params {
+  int32_t crop_kind;       /* 0 = get_random_crop, 1 = get_center_crop */
+  int32_t out_h, out_w;    /* needed for cutout bounds */
+  int32_t cutout_size;     /* 0 = no cutout draw */
+  double scale[2];         /* RandomResizedCrop scale (rgb_image.py:234) */
+  double ratio[2];         /* RandomResizedCrop ratio */
+  double center_ratio;     /* CenterCrop ratio (rgb_image.py:259) */
+  uint64_t loader_seed;
+  uint64_t epoch;
+  int32_t flip_prob_x1e6;  /* RandomHorizontalFlip p*1e6 (0 = none) */
+  int32_t reserved;
+} ffcv_draw_params;
+
+/* ---------------------------------------------------------------- misc -- */
+int ffcv_abi_version(void);
+const char *ffcv_last_error(void);
+int ffcv_device_count(int *count);
+int ffcv_set_device(int device);
+int ffcv_stream_synchronize(void *stream);
+
+/* Device memory helpers (for callers without torch; the Python package uses
+ * torch allocations instead). */
+int ffcv_malloc(void **dptr, uint64_t bytes);
+int ffcv_free(void *dptr);
+int ffcv_memcpy_h2d_async(void *dst, const void *src, uint64_t bytes, void *stream);
+int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stream);
+
+/* libffcv.cpp:44-46 my_memcpy (host plumbing; SimpleRGBImageDecoder raw on a
+ * CPU-only Loader, C1).  Same argument order as the reference. */
+void my_memcpy(void *source, void *dst, uint64_t size);
+
+/* ------------------------------------------------------- random draws -- */
+/* rgb_image.py:48-81 crop windows (+ cutout.py:38-42 origins, + flip.py:35
+ * decisions) for B samples, on the device.
+ *   sample_ids : device uint64[B] dataset indices (batch_indices)
+ *   samples    : device ffcv_sample[B] (height/width used)
+ *   crops      : device int32[B][4] (i, j, h, w) out
+ *   cutout_yx  : device int32[B][2] out, or NULL
+ *   flips      : device uint8[B] out, or NULL
+ *   status     : device int32[B] out, or NULL */
+int ffcv_draw_batch(void *stream, const uint64_t *sample_ids,
+                    const ffcv_sample *samples, int batch,
+                    const ffcv_draw_params *p, int32_t *crops,
+                    int32_t *cutout_yx, uint8_t *flips, int32_t *status);
+
+/* ------------------------------------------- raw-mode crop + resize ---- */
+/* rgb_image.py:202-208 (raw branch) + libffcv.cpp:33-42 cv::resize
+ * INTER_AREA, fused with Cutout (cutout.py:44) and the NormalizeImage LUT
+ * (normalize.py:65).  Samples with mode != raw are skipped.
+ *   base  : device pointer to the .beton bytes (file offset 0)
+ *   out   : device [B][out_h][out_w][3] uint8 (lut==NULL) or fp16 bits */
+int ffcv_rrc_raw_batch(void *stream, const uint8_t *base,
+                       const ffcv_sample *samples, int batch,
+                       const int32_t *crops, const int32_t *cutout_yx,
+                       const uint8_t *flips, const ffcv_rrc_params *p,
+                       void *out);
+
+/* Per-batch descriptor gather: out[k] = table[ids[k]] (the reference reads
+ * metadata[source_ix] per sample, rgb_image.py:188-189).  table: device
+ * ffcv_sample[N] built once per dataset; ids: device uint64[B]. */
+int ffcv_gather_samples(void *stream, const ffcv_sample *table, uint64_t n_table,
+                        const uint64_t *ids, int batch, ffcv_sample *out);
+
+/* rgb_image.py:123-136 SimpleRGBImageDecoder raw branch (my_memcpy per
+ * sample) as a device gather into [B][H][W][3]. */
+int ffcv_gather_raw_batch(void *stream, const uint8_t *base,
+                          const ffcv_sample *samples, int batch, uint8_t *out,
+                          uint64_t out_stride);
+
+/* ------------------------------------------------------- JPEG decode -- */
+/* Baseline-sequential Huffman JPEG, 8-bit, 1 or 3 components, any 1x/2x
+ * sampling, bit-exact with libjpeg-turbo tjDecompress2(TJPF_RGB,
+ * TJFLAG_FASTDCT) (libffcv.cpp:104-106): ifast IDCT, fancy upsampling,
+ * fixed-point YCbCr->RGB.  One context holds the scratch for up to
+ * max_batch images of at most max_height x max_width pixels and max_bytes
+ * compressed bytes each. */
+typedef struct ffcv_jpeg_ctx ffcv_jpeg_ctx;
+int ffcv_jpeg_create(ffcv_jpeg_ctx **ctx, int max_batch, uint32_t max_height,
+                     uint32_t max_width, uint64_t max_bytes);
+int ffcv_jpeg_destroy(ffcv_jpeg_ctx *ctx);
+
+/* rgb_image.py:185-210 jpg branch fused end to end: decode only the MCUs the
+ * crop needs -> crop -> INTER_AREA -> cutout -> LUT.  Samples with mode !=
+ * jpg are skipped (call ffcv_rrc_raw_batch for them).  status: device
+ * int32[B] (FFCV_SAMPLE_*), required. */
+int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *ctx, void *stream, const uint8_t *base,
+                        const ffcv_sample *samples, int batch,
+                        const int32_t *crops, const int32_t *cutout_yx,
+                        const uint8_t *flips, const ffcv_rrc_params *p,
+                        void *out, int32_t *status);
+
+/* rgb_image.py:123-136 SimpleRGBImageDecoder jpg branch (imdecode into the
+ * destination, full image) -> device [B][H][W][3] with out_stride bytes per
+ * sample. */
+int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *ctx, void *stream,
+                           const uint8_t *base, const ffcv_sample *samples,
+                           int batch, uint8_t *out, uint64_t out_stride,
+                           int32_t *status);
+
+/* Test hook: quantised coefficients (DC predicted, natural order) of every
+ * block in MCU order, [B][max_blocks][64] int16, for checking the entropy
+ * stage against the oracle on its own. */
+int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *ctx, void *stream,
+                                 const uint8_t *base,
+                                 const ffcv_sample *samples, int batch,
+                                 int16_t *coefs, uint64_t max_blocks,
+                                 int32_t *status);
+
+/* ---------------------------------------------- standalone transforms -- */
+/* cutout.py:36-47 in place on a device [B][H][W][3] uint8 batch. */
+int ffcv_cutout_batch(void *stream, uint8_t *images, int batch, int height,
+                      int width, const int32_t *cutout_yx, int crop_size,
+                      const uint8_t fill[3]);
+/* normalize.py:65 cupy kernel: out[i] = lut[in[i]*3 + i%3] over n elements
+ * of a channels-last uint8 batch; out holds fp16 bits. */
+int ffcv_normalize_batch(void *stream, const uint8_t *in, uint64_t n,
+                         const uint16_t *lut, uint16_t *out);
+/* flip.py:35-40: dst[i] = images[i, :, ::-1] where flips[i] != 0. */
+int ffcv_flip_batch(void *stream, const uint8_t *in, uint8_t *out, int batch,
+                    int height, int width, int channels_bytes,
+                    const uint8_t *flips);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

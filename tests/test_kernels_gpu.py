@@ -1,0 +1,316 @@
+"""GPU parity of the C-ABI kernels against the oracle (bit-exact).
+
+Each test drives libffcv_hip.so through its C ABI (ffcv_amd.libffcv) on
+cuda:0 and compares with the CPU restatement in oracle/ (itself pinned to
+libjpeg-turbo and to the reference's own Python, see test_oracle.py).
+"""
+import numpy as np
+import pytest
+
+from tests.imagegen import natural_image, encode_jpeg, pack, imagenet_like_shape
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    return torch
+
+
+def _upload(buf):
+    torch = _torch()
+    return torch.from_numpy(buf).to('cuda:0')
+
+
+def _samples(offs, sizes, hs, ws, modes):
+    from ffcv_amd.libffcv import SAMPLE_DTYPE
+    a = np.zeros(len(offs), SAMPLE_DTYPE)
+    a['offset'] = offs
+    a['size'] = sizes
+    a['height'] = hs
+    a['width'] = ws
+    a['mode'] = modes
+    return a
+
+
+def _dev(a):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to('cuda:0')
+
+
+def _draw(hip_lib, ids, hs, ws, seed, epoch, crop_kind=0, cutout=0, out=(224, 224), flip_p=0.0,
+          scale=(0.08, 1.0), ratio=(0.75, 4 / 3)):
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    B = len(ids)
+    smp = _samples(np.zeros(B, np.uint64), np.zeros(B, np.uint64), hs, ws, np.zeros(B))
+    d_smp = _dev(smp)
+    d_ids = torch.from_numpy(np.asarray(ids, np.uint64).view(np.int64)).to('cuda:0')
+    crops = torch.zeros((B, 4), dtype=torch.int32, device='cuda:0')
+    cut = torch.zeros((B, 2), dtype=torch.int32, device='cuda:0') if cutout else None
+    flips = torch.zeros(B, dtype=torch.uint8, device='cuda:0') if flip_p > 0 else None
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    p = L.DrawParams()
+    p.crop_kind = crop_kind
+    p.out_h, p.out_w = out
+    p.cutout_size = cutout
+    p.scale[0], p.scale[1] = scale
+    p.ratio[0], p.ratio[1] = ratio
+    p.center_ratio = 224 / 256
+    p.loader_seed = seed
+    p.epoch = epoch
+    p.flip_prob_x1e6 = int(round(flip_p * 1e6))
+    L.draw_batch(d_ids, d_smp, p, crops, cut, flips, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    return (crops.cpu().numpy(), cut.cpu().numpy() if cut is not None else None,
+            flips.cpu().numpy() if flips is not None else None)
+
+
+def test_draws_match_oracle(hip_lib, oracle):
+    rng = np.random.default_rng(3)
+    B = 20000
+    ids = rng.integers(0, 2 ** 40, B).astype(np.uint64)
+    hs = rng.integers(1, 1500, B).astype(np.uint32)
+    ws = rng.integers(1, 1500, B).astype(np.uint32)
+    for seed, epoch in [(0, 0), (1234, 7)]:
+        crops, cut, flips = _draw(hip_lib, ids, hs, ws, seed, epoch, cutout=32, flip_p=0.5)
+        ocrops, ocut = oracle.draw_batch(ids, hs, ws, seed, epoch, cutout_size=32)
+        assert np.array_equal(crops, ocrops), np.argwhere((crops != ocrops).any(1))[:5]
+        assert np.array_equal(cut, ocut)
+        oflip = np.array([oracle.MT(oracle.sample_seed(seed, epoch, int(i), 3)).uniform(0, 1) < 0.5
+                          for i in ids[:2000]])
+        assert np.array_equal(flips[:2000].astype(bool), oflip)
+    # center crop
+    crops, _, _ = _draw(hip_lib, ids[:3000], hs[:3000], ws[:3000], 0, 0, crop_kind=1)
+    ocrops, _ = oracle.draw_batch(ids[:3000], hs[:3000], ws[:3000], 0, 0, crop='center')
+    assert np.array_equal(crops, ocrops)
+
+
+def _run_raw_rrc(hip_lib, imgs, crops, out_hw, cut=None, cut_size=0, fill=(0, 0, 0), flips=None,
+                 lut=None, cut_before_flip=False):
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    blobs = [im.reshape(-1) for im in imgs]
+    buf, offs, sizes = pack(blobs)
+    smp = _samples(offs, sizes, [im.shape[0] for im in imgs], [im.shape[1] for im in imgs],
+                   np.ones(len(imgs)))
+    B = len(imgs)
+    d_buf, d_smp = _upload(buf), _dev(smp)
+    d_crops = torch.from_numpy(np.ascontiguousarray(crops, np.int32)).to('cuda:0')
+    d_cut = torch.from_numpy(np.ascontiguousarray(cut, np.int32)).to('cuda:0') if cut is not None else None
+    d_flips = torch.from_numpy(np.asarray(flips, np.uint8)).to('cuda:0') if flips is not None else None
+    p = L.RRCParams()
+    p.out_h, p.out_w = out_hw
+    p.cutout_size = cut_size
+    for i in range(3):
+        p.cutout_fill[i] = fill[i]
+    p.cutout_fill[3] = int(cut_before_flip)
+    d_lut = None
+    if lut is not None:
+        d_lut = torch.from_numpy(np.ascontiguousarray(lut).view(np.int16)).to('cuda:0')
+        p.lut = d_lut.data_ptr()
+        out = torch.zeros((B, out_hw[0], out_hw[1], 3), dtype=torch.float16, device='cuda:0')
+    else:
+        out = torch.zeros((B, out_hw[0], out_hw[1], 3), dtype=torch.uint8, device='cuda:0')
+    L.rrc_raw_batch(d_buf, d_smp, B, d_crops, d_cut, d_flips, p, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _oracle_post(u8, flips=None, cut=None, cut_size=0, fill=(0, 0, 0), lut=None, cut_before_flip=False):
+    u8 = u8.copy()
+    for k in range(u8.shape[0]):
+        if cut is not None and cut_before_flip:
+            y, x = cut[k]
+            u8[k, y:y + cut_size, x:x + cut_size] = fill
+        if flips is not None and flips[k]:
+            u8[k] = u8[k, :, ::-1]
+        if cut is not None and not cut_before_flip:
+            y, x = cut[k]
+            u8[k, y:y + cut_size, x:x + cut_size] = fill
+    if lut is not None:
+        idx = u8.astype(np.int64)
+        return np.stack([lut[idx[..., c], c] for c in range(3)], -1)
+    return u8
+
+
+def test_raw_rrc_matches_oracle(hip_lib, oracle):
+    rng = np.random.default_rng(11)
+    imgs, crops = [], []
+    shapes = [(512, 512), (300, 500), (500, 333), (224, 224), (256, 192), (64, 48), (1, 1),
+              (7, 900), (1000, 1000), (449, 449), (672, 448)]
+    for k in range(64):
+        h, w = shapes[k % len(shapes)] if k < 33 else (int(rng.integers(1, 700)), int(rng.integers(1, 700)))
+        imgs.append(natural_image(rng, h, w))
+    # crops: device draws + hand-picked exact-scale cases (copy, 2x, 3x)
+    ids = np.arange(len(imgs), dtype=np.uint64)
+    dc, cut, flips = _draw(hip_lib, ids, [i.shape[0] for i in imgs], [i.shape[1] for i in imgs], 5, 1,
+                           cutout=48, out=(224, 224), flip_p=0.5)
+    crops = dc.copy()
+    crops[3] = (0, 0, 224, 224)      # copy branch
+    crops[8] = (1, 1, 448, 448)      # 2x area-fast
+    crops[9] = (0, 0, 449, 449)      # general area
+    crops[10] = (0, 0, 672, 448)     # 3x / 2x integer scales
+    for k in range(11, len(imgs)):
+        h, w = imgs[k].shape[:2]
+        if k % 4 == 0:
+            crops[k] = (0, 0, h, w)  # full image: both branches by size
+    u8 = oracle.rrc_batch([(im.reshape(-1), im.shape[0], im.shape[1], 1) for im in imgs], crops, 224, 224)
+    got = _run_raw_rrc(hip_lib, imgs, crops, (224, 224))
+    bad = np.argwhere((got != u8).reshape(len(imgs), -1).any(1)).ravel()
+    assert bad.size == 0, f'samples {bad[:8]} differ; crops {crops[bad[:4]]}'
+    # fused epilogue: flip + cutout (both orders) + LUT
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    for cbf in (False, True):
+        got = _run_raw_rrc(hip_lib, imgs, crops, (224, 224), cut, 48, (124, 116, 103), flips, lut, cbf)
+        want = _oracle_post(u8, flips, cut, 48, (124, 116, 103), lut, cbf)
+        assert np.array_equal(got.view(np.uint16), want.view(np.uint16))
+
+
+def test_raw_rrc_448_c5(hip_lib, oracle):
+    rng = np.random.default_rng(5)
+    imgs = [natural_image(rng, 512, 512) for _ in range(16)]
+    crops, cut, _ = _draw(hip_lib, np.arange(16, dtype=np.uint64), [512] * 16, [512] * 16, 0, 0,
+                          cutout=64, out=(448, 448))
+    u8 = oracle.rrc_batch([(im.reshape(-1), 512, 512, 1) for im in imgs], crops, 448, 448,
+                          cutout_yx=cut, cutout_size=64)
+    got = _run_raw_rrc(hip_lib, imgs, crops, (448, 448), cut, 64)
+    assert np.array_equal(got, u8)
+
+
+def _jpeg_set(rng, n, max_side=256):
+    imgs, blobs = [], []
+    subs = ['4:2:0', '4:2:2', '4:4:4']
+    for k in range(n):
+        if k % 5 == 4:
+            h, w = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        else:
+            h, w = imagenet_like_shape(rng, max_side)
+        img = natural_image(rng, h, w)
+        if k % 17 == 16:
+            img = img[:, :, 0].copy()
+        q = [90, 95, 75, 50, 100][k % 5]
+        blobs.append(encode_jpeg(img, q, subs[k % 3]))
+        imgs.append(img)
+    return imgs, blobs
+
+
+def _jpeg_dev(blobs, imgs):
+    buf, offs, sizes = pack(blobs)
+    smp = _samples(offs, sizes, [i.shape[0] for i in imgs], [i.shape[1] for i in imgs], np.zeros(len(imgs)))
+    return _upload(buf), _dev(smp)
+
+
+def test_jpeg_full_decode_matches_libjpeg(hip_lib, oracle):
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(21)
+    imgs, blobs = _jpeg_set(rng, 60)
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    maxh = max(i.shape[0] for i in imgs)
+    maxw = max(i.shape[1] for i in imgs)
+    dec = L.JpegDecoder(B, maxh, maxw, max(len(b) for b in blobs))
+    stride = maxh * maxw * 3
+    out = torch.zeros(B * stride, dtype=torch.uint8, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.decode(d_buf, d_smp, B, out, stride, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    o = out.cpu().numpy()
+    for k in range(B):
+        assert st[k] == 0, (k, st[k])
+        h, w = imgs[k].shape[:2]
+        got = o[k * stride:k * stride + h * w * 3].reshape(h, w, 3)
+        want = oracle.jpeg_decode(blobs[k])
+        assert np.array_equal(got, want), f'sample {k} {imgs[k].shape}'
+        if k % 7 == 0:
+            assert np.array_equal(want, oracle.ljt_decode(blobs[k]))
+
+
+def test_jpeg_coefficients_match_oracle(hip_lib, oracle):
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(22)
+    imgs, blobs = _jpeg_set(rng, 40)
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    dec = L.JpegDecoder(B, 300, 300, max(len(b) for b in blobs))
+    maxb = 4000
+    out = torch.zeros((B, maxb, 64), dtype=torch.int16, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.coefficients(d_buf, d_smp, B, out, maxb, status)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    st = status.cpu().numpy()
+    for k in range(B):
+        want = oracle.jpeg_coefficients(blobs[k])
+        assert st[k] == 0
+        assert np.array_equal(o[k, :len(want)], want), f'sample {k}'
+
+
+def test_jpeg_rrc_matches_oracle(hip_lib, oracle):
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(23)
+    imgs, blobs = _jpeg_set(rng, 96)
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    hs = [i.shape[0] for i in imgs]
+    ws = [i.shape[1] for i in imgs]
+    crops, cut, flips = _draw(hip_lib, np.arange(B, dtype=np.uint64) + 1000, hs, ws, 9, 2, cutout=32,
+                              flip_p=0.5)
+    dec = L.JpegDecoder(B, max(hs), max(ws), max(len(b) for b in blobs))
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    u8 = oracle.rrc_batch([(b, h, w, 0) for b, h, w in zip(blobs, hs, ws)], crops, 224, 224)
+    d_crops = torch.from_numpy(crops).to('cuda:0')
+    d_cut = torch.from_numpy(cut).to('cuda:0')
+    d_flips = torch.from_numpy(flips).to('cuda:0')
+    d_lut = torch.from_numpy(lut.view(np.int16)).to('cuda:0')
+    for use_lut in (False, True):
+        p = L.RRCParams()
+        p.out_h, p.out_w = 224, 224
+        p.cutout_size = 32
+        for i, f in enumerate((124, 116, 103)):
+            p.cutout_fill[i] = f
+        if use_lut:
+            p.lut = d_lut.data_ptr()
+        out = torch.zeros((B, 224, 224, 3), dtype=torch.float16 if use_lut else torch.uint8, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        dec.rrc(d_buf, d_smp, B, d_crops, d_cut, d_flips, p, out, status)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == 0).all()
+        want = _oracle_post(u8, flips, cut, 32, (124, 116, 103), lut if use_lut else None)
+        got = out.cpu().numpy()
+        bad = np.argwhere((got.view(np.uint8) != want.view(np.uint8)).reshape(B, -1).any(1)).ravel()
+        assert bad.size == 0, f'samples {bad[:8]} differ'
+
+
+def test_jpeg_corrupt_and_unsupported(hip_lib, oracle):
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    from PIL import Image
+    import io
+    rng = np.random.default_rng(1)
+    img = natural_image(rng, 64, 80)
+    good = encode_jpeg(img)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, format='JPEG', progressive=True)
+    prog = np.frombuffer(b.getvalue(), np.uint8)
+    junk = rng.integers(0, 256, 500).astype(np.uint8)
+    blobs = [good, prog, junk, good[:40]]
+    imgs = [img] * 4
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    dec = L.JpegDecoder(4, 64, 80, 100000)
+    out = torch.full((4, 64 * 80 * 3), 7, dtype=torch.uint8, device='cuda:0')
+    status = torch.full((4,), -1, dtype=torch.int32, device='cuda:0')
+    dec.decode(d_buf, d_smp, 4, out, 64 * 80 * 3, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert st[0] == 0 and st[1] == 2 and st[2] == 1 and st[3] != 0
+    o = out.cpu().numpy()
+    assert np.array_equal(o[0].reshape(64, 80, 3), oracle.jpeg_decode(good))
+    assert (o[1] == 0).all() and (o[2] == 0).all()

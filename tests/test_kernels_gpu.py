@@ -7,7 +7,7 @@ libjpeg-turbo and to the reference's own Python, see test_oracle.py).
 import numpy as np
 import pytest
 
-from tests.imagegen import natural_image, encode_jpeg, pack, imagenet_like_shape
+from ffcv_amd.synthetic import natural_image, encode_jpeg, pack, imagenet_like_shape
 
 pytestmark = pytest.mark.gpu
 

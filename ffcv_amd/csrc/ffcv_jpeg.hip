@@ -436,7 +436,15 @@ struct JpegArgs {
   uint64_t roi_slot;
   uint32_t max_h, max_w;
   uint64_t max_blocks;  // JM_COEF output capacity
+  uint64_t *dbg;        // optional per-image phase stamps (diagnostic builds)
 };
+
+// Diagnostic stamps: lane 0 records s_memtime at phase boundaries into
+// dbg[image*16 + slot] (never read by the kernel; off when dbg == nullptr).
+#define STAMP(slot)                                                          \
+  do {                                                                       \
+    if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + (slot)] = wall_clock64();  \
+  } while (0)
 
 struct RoiScratch {
   const uint8_t *p;
@@ -455,6 +463,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   const uint32_t nbytes = (uint32_t)smp.size;
 
   // ------------------------------------------------------------- P0 ----
+  STAMP(0);
   if (t == 0) {
     int st = FFCV_SAMPLE_OK;
     for (int i = 0; i < 4; i++) S.dqt_ok[i] = 0;
@@ -713,6 +722,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   }
 
   // ------------------------------------------------------------- P1 ----
+  STAMP(1);
   if (t < NTAB) {
     if (S.dht_ok[t]) {
       HuffTab &T = S.tab[t];
@@ -775,6 +785,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   }
 
   // ------------------------------------------------------------- P2 ----
+  STAMP(2);
   // entropy-coded segment: [scan_off, first marker)
   const uint32_t seg0 = S.scan_off;
   const uint32_t seglen = nbytes > seg0 ? nbytes - seg0 : 0;
@@ -814,6 +825,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   const uint32_t total_bits = dlen * 8;
 
   // ------------------------------------------------------------- P3 ----
+  STAMP(3);
   if (t == 0) {
     // at least ~192 bits per lane so resynchronisation is cheap relative to work
     uint32_t nthr = (total_bits + 191) / 192;
@@ -849,7 +861,10 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
       changed = ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph;
     }
     int anyc = __syncthreads_or(changed);
-    if (!anyc) break;
+    if (!anyc) {
+      if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + 12] = (uint64_t)round;
+      break;
+    }
     if (changed) {
       g = ng;
       my_dc[0] = my_dc[1] = my_dc[2] = 0;
@@ -867,6 +882,8 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   }
 
   // ------------------------------------------------------------- P4 ----
+  STAMP(4);
+  if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + 13] = (uint64_t)nthr;
   const uint32_t blk_base = wg_exscan_u32(my_cnt, S.scan_tmp);
   int32_t pred[3];
   for (int c = 0; c < 3; c++) pred[c] = wg_exscan_i32(my_dc[c], S.scan_tmp2[c]);
@@ -880,6 +897,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   }
 
   // ------------------------------------------------------------- P5 ----
+  STAMP(5);
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
     if (cur >= 0)
@@ -904,6 +922,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   }
 
   // ------------------------------------------------------------- P6 ----
+  STAMP(6);
   uint8_t *planes = a.planes + a.plane_slot * k;
   for (int c = 0; c < S.ncomp; c++) {
     int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
@@ -920,6 +939,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   __syncthreads();
 
   // ------------------------------------------------------------- P7 ----
+  STAMP(7);
   const int rh = S.rh, rw = S.rw, ri = S.ri, rj = S.rj;
   uint8_t *roi;
   uint64_t roi_step;
@@ -962,6 +982,7 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   __syncthreads();
 
   // ------------------------------------------------------------- P8 ----
+  STAMP(8);
   __shared__ uint16_t s_lut[FP16 ? 768 : 1];
   if (FP16) {
     for (int i = t; i < 768; i += JT) s_lut[i] = a.p.lut[i];
@@ -1004,11 +1025,13 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
       o[2] = (uint8_t)v[2];
     }
   }
+  STAMP(9);
   if (t == 0 && !S.any) a.status[k] = FFCV_SAMPLE_OK;
 }
 
 // ---------------------------------------------------------------- ctx -----
 struct ffcv_jpeg_ctx {
+  uint64_t *dbg;
   int max_batch;
   uint32_t max_h, max_w;
   uint64_t max_bytes;
@@ -1062,6 +1085,14 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
   return FFCV_OK;
 }
 
+// Diagnostic hook (not in the public header): per-image phase stamps
+// (wall_clock64, 100 MHz) into dbg[B][16]; NULL disables.
+int ffcv_jpeg_set_debug(ffcv_jpeg_ctx *c, uint64_t *dbg) {
+  if (!c) return FFCV_EINVAL;
+  c->dbg = dbg;
+  return FFCV_OK;
+}
+
 int ffcv_jpeg_destroy(ffcv_jpeg_ctx *c) {
   if (!c) return FFCV_OK;
   (void)hipFree(c->dstuff);
@@ -1087,6 +1118,7 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.roi_slot = c->roi_slot;
   a.max_h = c->max_h;
   a.max_w = c->max_w;
+  a.dbg = c->dbg;
   return a;
 }
 

@@ -1,0 +1,51 @@
+"""Diagnostic: per-phase timing of jpeg_kernel<RRC> via in-kernel stamps.
+
+Runs one batch with the debug stamp buffer enabled (diagnostic only: the
+stamps are written to their own buffer and never read by the kernel).
+"""
+import ctypes, os, sys, time
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from ffcv_amd import libffcv as L
+from bench import make_unique, IMAGENET_MEAN, IMAGENET_STD
+from ffcv_amd.transforms.lut import make_lut
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+tile, offs, sizes, hs, ws = make_unique('jpg', 256, 4096, 0, 16)
+dev = torch.device('cuda:0')
+d_data = torch.from_numpy(tile).to(dev)
+idx = np.random.default_rng(1).permutation(len(offs))[:B]
+smp = np.zeros(B, L.SAMPLE_DTYPE)
+smp['offset'] = offs[idx]; smp['size'] = sizes[idx]; smp['height'] = hs[idx]; smp['width'] = ws[idx]
+d_smp = torch.from_numpy(smp.view(np.uint8)).to(dev)
+d_ids = torch.from_numpy(idx.astype(np.int64)).to(dev)
+crops = torch.empty((B, 4), dtype=torch.int32, device=dev)
+cut = torch.empty((B, 2), dtype=torch.int32, device=dev)
+dp = L.DrawParams(); dp.out_h = dp.out_w = 224; dp.cutout_size = 32
+dp.scale[0], dp.scale[1] = 0.08, 1.0; dp.ratio[0], dp.ratio[1] = 0.75, 4/3
+L.draw_batch(d_ids, d_smp, dp, crops, cut, None, None)
+lut = torch.from_numpy(make_lut(IMAGENET_MEAN, IMAGENET_STD).view(np.int16)).to(dev)
+rp = L.RRCParams(); rp.out_h = rp.out_w = 224; rp.cutout_size = 32; rp.lut = lut.data_ptr()
+out = torch.empty((B, 224, 224, 3), dtype=torch.float16, device=dev)
+status = torch.empty(B, dtype=torch.int32, device=dev)
+dec = L.JpegDecoder(B, 256, 256, int(sizes.max()))
+dbg = torch.zeros((B, 16), dtype=torch.int64, device=dev)
+L.lib().ffcv_jpeg_set_debug.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+for it in range(3):
+    L.lib().ffcv_jpeg_set_debug(dec.handle, ctypes.c_void_p(dbg.data_ptr() if it == 2 else 0))
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    dec.rrc(d_data, d_smp, B, crops, cut, None, rp, out, status)
+    torch.cuda.synchronize(); print('iter', it, 'ms', (time.perf_counter() - t0) * 1e3)
+d = dbg.cpu().numpy()
+names = ['parse', 'tables+zero', 'destuff', 'sync', 'scan', 'write', 'idct', 'color', 'resize']
+print('phase means (us):')
+for i, n in enumerate(names):
+    dt = (d[:, i + 1] - d[:, i]) / 100.0
+    print(f'  {n:12s} mean {dt.mean():8.1f}  p50 {np.median(dt):8.1f}  max {dt.max():8.1f}')
+tot = (d[:, 9] - d[:, 0]) / 100.0
+print('  total        mean', tot.mean(), 'max', tot.max())
+print('span of batch us', (d[:, 9].max() - d[:, 0].min()) / 100.0)
+print('rounds hist', np.bincount(d[:, 12].astype(int))[:20], 'nthr mean', d[:, 13].mean())
+st = (d[:, 0] - d[:, 0].min()) / 100.0
+print('start offsets us: p50', np.median(st), 'max', st.max())

@@ -1,2 +1,12 @@
-"""ffcv_amd: MI355X-native drop-in for ffcv's image decode-and-augment path."""
+"""ffcv_amd: MI355X-native drop-in for ffcv's image decode-and-augment path.
+
+``import ffcv_amd as ffcv`` gives the reference's public API surface for this
+path: ``Loader``, ``DatasetWriter``, ``fields``, ``transforms``,
+``pipeline`` (Operation / State / AllocationQuery), ``traversal_order``.
+"""
 __version__ = "0.1.0"
+
+from .loader import Loader  # noqa: E402
+from .writer import DatasetWriter  # noqa: E402
+
+__all__ = ['Loader', 'DatasetWriter']

@@ -458,7 +458,10 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   const int t = threadIdx.x;
   const int k = blockIdx.x;
   const ffcv_sample smp = a.samples[k];
-  if (smp.mode != 0) return;
+  if (smp.mode != 0) {  // raw samples are handled by rrc_raw_kernel / gather
+    if (t == 0) a.status[k] = FFCV_SAMPLE_OK;
+    return;
+  }
   const uint8_t *src = a.base + smp.offset;
   const uint32_t nbytes = (uint32_t)smp.size;
 

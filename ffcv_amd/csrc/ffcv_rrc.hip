@@ -19,10 +19,10 @@ __global__ void __launch_bounds__(64) draw_kernel(const uint64_t *__restrict__ i
   int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= B) return;
   uint64_t id = ids[k];
-  uint32_t H = samples[k].height, W = samples[k].width;
   int err = 0;
   DevMT m;
   if (crops) {
+    uint32_t H = samples[k].height, W = samples[k].width;
     int32_t c[4];
     if (p.crop_kind == 0) {
       mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 1));
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(64) draw_kernel(const uint64_t *__restrict__ i
     // flip.py:35 rand() < flip_prob, one draw per sample under the contract
     mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 3));
     double u = mt_double(m);
-    flips[k] = (uint8_t)(u < (double)p.flip_prob_x1e6 * 1e-6);
+    flips[k] = (uint8_t)(u < p.flip_prob);
   }
   if (status) status[k] = err ? FFCV_SAMPLE_RNG : FFCV_SAMPLE_OK;
 }
@@ -215,7 +215,7 @@ extern "C" {
 int ffcv_draw_batch(void *stream, const uint64_t *sample_ids, const ffcv_sample *samples, int batch,
                     const ffcv_draw_params *p, int32_t *crops, int32_t *cutout_yx, uint8_t *flips,
                     int32_t *status) {
-  if (batch < 0 || !p || !sample_ids || !samples) {
+  if (batch < 0 || !p || !sample_ids || (crops && !samples)) {
     ffcv::set_error("ffcv_draw_batch: invalid arguments");
     return FFCV_EINVAL;
   }

@@ -57,7 +57,7 @@ class DrawParams(ctypes.Structure):
                 ('cutout_size', c_int32), ('scale', ctypes.c_double * 2),
                 ('ratio', ctypes.c_double * 2), ('center_ratio', ctypes.c_double),
                 ('loader_seed', c_uint64), ('epoch', c_uint64),
-                ('flip_prob_x1e6', c_int32), ('reserved', c_int32)]
+                ('flip_prob', ctypes.c_double)]
 
 
 _lib = None

@@ -1,0 +1,260 @@
+"""FFCV Loader, MI355X edition (ffcv/loader/loader.py:30-278).
+
+Same constructor, options, ordering, ``__len__``, ``filter`` and epoch
+semantics as the reference.  Differences:
+
+* the decode-and-augment stages run on a HIP device (the device of the
+  pipelines' ``ToDevice``, else the current device) as kernels enqueued on
+  per-slot streams; there is no numba;
+* ``device_cache=True`` (default when a GPU is present) copies the whole
+  ``.beton`` into HBM once and decodes from there; ``device_cache=False``
+  gathers each batch's compressed bytes into pinned host memory and copies
+  them in (the PCIe-inclusive path);
+* augmentation randomness follows the per-sample seeding contract
+  (DESIGN.md): results depend only on (seed, epoch, sample index), not on
+  thread scheduling.
+"""
+from collections.abc import Sequence as SeqABC
+from enum import Enum, unique, auto
+from os import environ, sched_getaffinity
+from typing import Any, Callable, Mapping, Sequence, Type, Union
+
+import numpy as np
+import torch as ch
+
+from .epoch_iterator import EpochIterator
+from ..reader import Reader
+from ..traversal_order.base import TraversalOrder
+from ..traversal_order import Random, Sequential, QuasiRandom
+from ..pipeline import PipelineSpec, Compiler
+from ..pipeline.operation import Operation
+from ..pipeline.graph import Graph
+from ..pipeline.runtime import DeviceDataset
+from ..memory_managers import ProcessCacheManager, OSCacheManager, MemoryManager
+from ..fields.base import Field
+
+
+@unique
+class OrderOption(Enum):
+    SEQUENTIAL = auto()
+    RANDOM = auto()
+    QUASI_RANDOM = auto()
+
+
+ORDER_TYPE = Union[TraversalOrder, OrderOption]
+
+ORDER_MAP = {
+    OrderOption.RANDOM: Random,
+    OrderOption.SEQUENTIAL: Sequential,
+    OrderOption.QUASI_RANDOM: QuasiRandom,
+}
+
+DEFAULT_PROCESS_CACHE = int(environ.get('FFCV_DEFAULT_CACHE_PROCESS', "0"))
+DEFAULT_OS_CACHE = not DEFAULT_PROCESS_CACHE
+
+
+def _infer_device(pipelines):
+    from ..transforms.ops import ToDevice
+    for spec in pipelines.values():
+        ops = spec if isinstance(spec, SeqABC) else (getattr(spec, 'transforms', None) or [])
+        for op in ops or []:
+            if isinstance(op, ToDevice):
+                d = ch.device(op.device)
+                if d.type == 'cuda':
+                    if d.index is None:
+                        d = ch.device('cuda', ch.cuda.current_device())
+                    return d
+    if ch.cuda.is_available():
+        return ch.device('cuda', ch.cuda.current_device())
+    return ch.device('cpu')
+
+
+class Loader:
+    """FFCV loader class that can be used as a drop-in replacement for
+    standard (e.g. PyTorch) data loaders.
+
+    Parameters
+    ----------
+    fname: str
+        Full path to the location of the dataset (.beton file format).
+    batch_size : int
+        Batch size.
+    num_workers : int
+        Host threads for host-side operations (torch intra-op threads).
+    os_cache : bool
+        Use the OS page cache for host reads (the only host reader here).
+    order : Union[OrderOption, TraversalOrder]
+        Traversal order: SEQUENTIAL, RANDOM, QUASI_RANDOM or a custom one.
+    distributed : bool
+        Emulates torch DistributedSampler (one process per GPU).
+    seed : int
+        Random seed for batch ordering (and the augmentation contract).
+    indices : Sequence[int]
+        Subset of dataset by filtering only some indices.
+    pipelines : Mapping[str, Sequence[Union[Operation, torch.nn.Module]]]
+        Per-field decoder + transforms; missing fields use the default
+        pipeline, ``None`` disables a field.
+    custom_fields : Mapping[str, Field]
+        Types of fields using a custom type.
+    drop_last : bool
+        Drop non-full batch in each iteration.
+    batches_ahead : int
+        Number of batches prepared in advance.
+    recompile : bool
+        Regenerate the schedule every epoch.
+    device : torch.device, optional (keyword only, new)
+        Decode device; default: the pipelines' ToDevice target, else the
+        current HIP device, else CPU (raw plumbing only).
+    device_cache : bool (keyword only, new)
+        Keep the whole .beton resident in HBM (default) or stage each
+        batch's bytes through pinned memory.
+    """
+
+    def __init__(self, fname: str, batch_size: int, num_workers: int = -1,
+                 os_cache: bool = DEFAULT_OS_CACHE,
+                 order: Union[ORDER_TYPE, TraversalOrder] = OrderOption.SEQUENTIAL,
+                 distributed: bool = False, seed: int = None, indices: Sequence[int] = None,
+                 pipelines: Mapping[str, Sequence[Union[Operation, ch.nn.Module]]] = {},
+                 custom_fields: Mapping[str, Type[Field]] = {}, drop_last: bool = True,
+                 batches_ahead: int = 3, recompile: bool = False, order_kwargs: dict = dict(),
+                 *, device=None, device_cache: bool = True):
+        if distributed and order == OrderOption.RANDOM and (seed is None):
+            print('Warning: no ordering seed was specified with distributed=True. '
+                  'Setting seed to 0 to match PyTorch distributed sampler.')
+            seed = 0
+        elif seed is None:
+            tinfo = np.iinfo('int32')
+            seed = np.random.randint(0, tinfo.max)
+        self._args = {
+            'fname': fname, 'batch_size': batch_size, 'num_workers': num_workers,
+            'os_cache': os_cache, 'order': order, 'distributed': distributed, 'seed': seed,
+            'indices': indices, 'pipelines': pipelines, 'drop_last': drop_last,
+            'batches_ahead': batches_ahead, 'recompile': recompile, 'device': device,
+            'device_cache': device_cache, 'custom_fields': custom_fields,
+        }
+        self.fname: str = fname
+        self.batch_size: int = batch_size
+        self.batches_ahead = batches_ahead
+        self.seed: int = seed
+        self.reader: Reader = Reader(self.fname, custom_fields)
+        self.num_workers: int = num_workers
+        self.drop_last: bool = drop_last
+        self.distributed: bool = distributed
+        self.code = None
+        self.recompile = recompile
+        if self.num_workers < 1:
+            self.num_workers = len(sched_getaffinity(0))
+        Compiler.set_num_threads(self.num_workers)
+
+        if indices is None:
+            self.indices = np.arange(self.reader.num_samples, dtype='uint64')
+        else:
+            self.indices = np.array(indices)
+
+        if os_cache:
+            self.memory_manager: MemoryManager = OSCacheManager(self.reader)
+        else:
+            self.memory_manager: MemoryManager = ProcessCacheManager(self.reader)
+
+        if order in ORDER_MAP:
+            self.traversal_order: TraversalOrder = ORDER_MAP[order](self)
+        elif isinstance(order, type) and issubclass(order, TraversalOrder):
+            self.traversal_order: TraversalOrder = order(self, **order_kwargs)
+        else:
+            raise ValueError(f"Order {order} is not a supported order type or a subclass of TraversalOrder")
+
+        memory_read = self.memory_manager.compile_reader()
+        self.next_epoch: int = 0
+
+        self.device = ch.device(device) if device is not None else _infer_device(pipelines)
+        if self.device.type == 'cuda':
+            from .. import libffcv
+            libffcv.lib()  # fail loudly now if the HIP library is missing
+            ch.cuda.set_device(self.device)
+            data = None
+            if device_cache:
+                from ..memory_managers.device_cache import upload_file
+                data = upload_file(self.fname, self.device)
+            self.device_dataset = DeviceDataset(self.reader, self.memory_manager, self.device, data)
+            if data is None:
+                self.device_dataset.staged = True
+        else:
+            self.device_dataset = None
+
+        self.pipelines = {}
+        self.pipeline_specs = {}
+        self.field_name_to_f_ix = {}
+        custom_pipeline_specs = {}
+        for output_name, spec in pipelines.items():
+            if isinstance(spec, PipelineSpec):
+                pass
+            elif isinstance(spec, SeqABC):
+                spec = PipelineSpec(output_name, decoder=None, transforms=spec)
+            elif spec is None:
+                continue
+            else:
+                raise ValueError(f"The pipeline for {output_name} has to be "
+                                 f"either a PipelineSpec or a sequence of operations")
+            custom_pipeline_specs[output_name] = spec
+
+        for f_ix, (field_name, field) in enumerate(self.reader.handlers.items()):
+            self.field_name_to_f_ix[field_name] = f_ix
+            if field_name not in custom_pipeline_specs:
+                if field_name not in pipelines:
+                    self.pipeline_specs[field_name] = PipelineSpec(field_name)
+            else:
+                self.pipeline_specs[field_name] = custom_pipeline_specs[field_name]
+        for field_name, spec in custom_pipeline_specs.items():
+            if field_name not in self.pipeline_specs:
+                self.pipeline_specs[field_name] = spec
+
+        self.graph = Graph(self.pipeline_specs, self.reader.handlers, self.field_name_to_f_ix,
+                           self.reader.metadata, memory_read, self.device)
+        self.generate_code()
+        self.first_traversal_order = self.next_traversal_order()
+
+    def next_traversal_order(self):
+        return self.traversal_order.sample_order(self.next_epoch)
+
+    def __iter__(self):
+        Compiler.set_num_threads(self.num_workers)
+        order = self.next_traversal_order()
+        selected_order = order[:len(self) * self.batch_size]
+        self.next_epoch += 1
+        if self.code is None or self.recompile:
+            self.generate_code()
+        return EpochIterator(self, selected_order)
+
+    def filter(self, field_name: str, condition: Callable[[Any], bool]) -> 'Loader':
+        new_args = {**self._args}
+        pipelines = {}
+        for other_field_name in self.reader.handlers.keys():
+            pipelines[other_field_name] = None
+        try:
+            pipelines[field_name] = new_args['pipelines'][field_name]
+        except KeyError:
+            del pipelines[field_name]
+        new_args['pipelines'] = pipelines
+        new_args['order'] = OrderOption.SEQUENTIAL
+        new_args['drop_last'] = False
+        sub_loader = Loader(**new_args)
+        selected_indices = []
+        for i, (batch,) in enumerate(sub_loader):
+            for j, sample in enumerate(batch):
+                sample_id = i * self.batch_size + j
+                if condition(sample):
+                    selected_indices.append(sample_id)
+        final_args = {**self._args}
+        final_args['indices'] = np.array(selected_indices)
+        return Loader(**final_args)
+
+    def __len__(self):
+        next_order = self.first_traversal_order
+        if self.drop_last:
+            return len(next_order) // self.batch_size
+        return int(np.ceil(len(next_order) / self.batch_size))
+
+    def generate_code(self):
+        self.graph._finalized = False
+        queries, code = self.graph.collect_requirements()
+        self.code = self.graph.codegen_all(code)

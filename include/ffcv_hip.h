@@ -89,8 +89,7 @@ typedef struct ffcv_draw_params {
   double center_ratio;     /* CenterCrop ratio (rgb_image.py:259) */
   uint64_t loader_seed;
   uint64_t epoch;
-  int32_t flip_prob_x1e6;  /* RandomHorizontalFlip p*1e6 (0 = none) */
-  int32_t reserved;
+  double flip_prob;        /* RandomHorizontalFlip probability (flip.py:33) */
 } ffcv_draw_params;
 
 /* ---------------------------------------------------------------- misc -- */
@@ -115,7 +114,8 @@ void my_memcpy(void *source, void *dst, uint64_t size);
 /* rgb_image.py:48-81 crop windows (+ cutout.py:38-42 origins, + flip.py:35
  * decisions) for B samples, on the device.
  *   sample_ids : device uint64[B] dataset indices (batch_indices)
- *   samples    : device ffcv_sample[B] (height/width used)
+ *   samples    : device ffcv_sample[B] (height/width used; may be NULL when
+ *                crops is NULL)
  *   crops      : device int32[B][4] (i, j, h, w) out
  *   cutout_yx  : device int32[B][2] out, or NULL
  *   flips      : device uint8[B] out, or NULL

@@ -61,7 +61,7 @@ def _draw(hip_lib, ids, hs, ws, seed, epoch, crop_kind=0, cutout=0, out=(224, 22
     p.center_ratio = 224 / 256
     p.loader_seed = seed
     p.epoch = epoch
-    p.flip_prob_x1e6 = int(round(flip_p * 1e6))
+    p.flip_prob = float(flip_p)
     L.draw_batch(d_ids, d_smp, p, crops, cut, flips, status)
     torch.cuda.synchronize()
     assert (status.cpu().numpy() == 0).all()

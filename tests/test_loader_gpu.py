@@ -1,0 +1,233 @@
+"""End-to-end Loader on the MI355X vs the oracle (bit-exact), through the
+reference's own API: Loader + pipelines of Operations.
+
+Ports the assertion intent of the reference suites (test_rrc.py,
+test_image_pipeline.py, test_image_normalization.py, test_image_read.py)
+and fixes the no-op ``is_true`` of test_rrc.py:65 into a real check; the
+full-pixel parity tests compare every output against the CPU restatement
+under the same (seed, epoch, sample index) contract.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch as ch
+
+from ffcv_amd.loader import Loader, OrderOption
+from ffcv_amd.reader import Reader
+from ffcv_amd.fields import RGBImageField, IntField
+from ffcv_amd.fields.decoders import (RandomResizedCropRGBImageDecoder, CenterCropRGBImageDecoder,
+                                      SimpleRGBImageDecoder, IntDecoder)
+from ffcv_amd.transforms import (ToTensor, ToDevice, ToTorchImage, NormalizeImage, Cutout,
+                                 RandomHorizontalFlip, Convert)
+from ffcv_amd.loader.epoch_iterator import DecodeError
+from tests.helpers import ConstDS, NaturalDS, write
+
+pytestmark = pytest.mark.gpu
+MEAN = np.array([0.485, 0.456, 0.406]) * 255
+STD = np.array([0.229, 0.224, 0.225]) * 255
+
+
+@pytest.fixture(scope='module', autouse=True)
+def need_gpu(hip_lib):
+    if not ch.cuda.is_available():
+        pytest.skip('no HIP device')
+
+
+@pytest.fixture(scope='module')
+def tmpdir_m():
+    return tempfile.mkdtemp()
+
+
+def _samples(fn):
+    r = Reader(fn)
+    mm = np.memmap(fn, np.uint8, mode='r')
+    sizes = dict(zip(r.alloc_table['ptr'].tolist(), r.alloc_table['size'].tolist()))
+    out = []
+    for md in r.metadata['f0']:
+        p = int(md['data_ptr'])
+        out.append((np.array(mm[p:p + sizes[p]]), int(md['height']), int(md['width']), int(md['mode'])))
+    return out
+
+
+def _expected(oracle, samples, ids, seed, epoch, out_hw, crop='random', ratio=224 / 256,
+              cutout=0, fill=(0, 0, 0), flip_p=0.0, cut_before_flip=False, lut=None):
+    ids = np.asarray(ids, np.uint64)
+    hs = [samples[int(i)][1] for i in ids]
+    ws = [samples[int(i)][2] for i in ids]
+    crops, cyx = oracle.draw_batch(ids, hs, ws, seed, epoch, crop=crop, center_ratio=ratio,
+                                   out_h=out_hw[0], out_w=out_hw[1], cutout_size=cutout)
+    u8 = oracle.rrc_batch([samples[int(i)] for i in ids], crops, out_hw[0], out_hw[1])
+    for k, sid in enumerate(ids):
+        if cutout and cut_before_flip:
+            y, x = cyx[k]
+            u8[k, y:y + cutout, x:x + cutout] = fill
+        if flip_p and oracle.MT(oracle.sample_seed(seed, epoch, int(sid), 3)).uniform(0, 1) < flip_p:
+            u8[k] = u8[k, :, ::-1]
+        if cutout and not cut_before_flip:
+            y, x = cyx[k]
+            u8[k, y:y + cutout, x:x + cutout] = fill
+    if lut is not None:
+        idx = u8.astype(np.int64)
+        return np.stack([lut[idx[..., c], c] for c in range(3)], -1)
+    return u8
+
+
+@pytest.mark.parametrize('mode', ['raw', 'jpg'])
+@pytest.mark.parametrize('decoder', ['rrc', 'cc'])
+def test_crop_decoders_constant_images(tmpdir_m, mode, decoder):
+    """test_rrc.py:52-110 (500 images 300-500 px, 160x160 output), with the
+    jpg branch actually asserted (the reference's is a no-op)."""
+    fn = os.path.join(tmpdir_m, f'const_{mode}.beton')
+    if not os.path.exists(fn):
+        write(fn, ConstDS(500, size_range=(300, 500)),
+              {'index': IntField(), 'value': RGBImageField(write_mode=mode, jpeg_quality=95)})
+    dec = RandomResizedCropRGBImageDecoder((160, 160)) if decoder == 'rrc' else \
+        CenterCropRGBImageDecoder((160, 160), 224 / 256)
+    loader = Loader(fn, batch_size=5, num_workers=2, pipelines={'value': [dec, ToTensor()]})
+    n = 0
+    for index, images in loader:
+        assert images.device.type == 'cpu'  # no ToDevice -> host tensor, like the reference
+        for i, image in zip(index, images):
+            assert image.shape == (160, 160, 3)
+            assert ch.all(image == (int(i) % 255)), int(i)
+            n += 1
+    assert n == 500
+
+
+@pytest.mark.parametrize('mode', ['raw', 'jpg'])
+def test_simple_pipeline_constant_images(tmpdir_m, mode):
+    """test_image_pipeline.py: 500x300 constant images (jpg q95) decode exactly."""
+    fn = os.path.join(tmpdir_m, f'simple_{mode}.beton')
+    write(fn, ConstDS(60, hw=(500, 300)),
+          {'index': IntField(), 'value': RGBImageField(write_mode=mode, jpeg_quality=95)})
+    loader = Loader(fn, batch_size=5, pipelines={'value': [SimpleRGBImageDecoder(), ToTensor(),
+                                                            ToDevice(ch.device('cuda:0'))]})
+    for index, images in loader:
+        assert images.device.type == 'cuda'
+        for i, image in zip(index, images):
+            assert ch.all(image == (int(i) % 255))
+
+
+def test_simple_jpeg_natural_matches_oracle(tmpdir_m, oracle):
+    fn = os.path.join(tmpdir_m, 'simple_nat.beton')
+    write(fn, NaturalDS(40, hw=(77, 131)), {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    samples = _samples(fn)
+    loader = Loader(fn, batch_size=8, order=OrderOption.RANDOM, seed=3,
+                    pipelines={'image': [SimpleRGBImageDecoder(), ToTensor(), ToDevice('cuda:0')],
+                               'label': [IntDecoder(), ToTensor(), ToDevice('cuda:0')]})
+    for images, labels in loader:
+        assert labels.device.type == 'cuda'
+        ids = None
+        imgs = images.cpu().numpy()
+        for k in range(imgs.shape[0]):
+            matches = [i for i, s in enumerate(samples)
+                       if np.array_equal(oracle.jpeg_decode(s[0]), imgs[k])]
+            assert matches and int(labels[k]) == matches[0] % 10
+
+
+@pytest.mark.parametrize('mode', ['raw', 'jpg'])
+def test_c3_pipeline_matches_oracle(tmpdir_m, oracle, mode):
+    """The north-star pipeline, fused into one launch, vs the oracle."""
+    fn = os.path.join(tmpdir_m, f'nat_{mode}.beton')
+    write(fn, NaturalDS(96, hw=(120, 160), var=True, seed=4),
+          {'image': RGBImageField(write_mode=mode, jpeg_quality=90), 'label': IntField()})
+    samples = _samples(fn)
+    lut = oracle.normalize_lut(MEAN, STD)
+    seed = 17
+    loader = Loader(fn, batch_size=32, order=OrderOption.RANDOM, seed=seed, pipelines={
+        'image': [RandomResizedCropRGBImageDecoder((64, 64)), Cutout(12, (124, 116, 103)), ToTensor(),
+                  ToDevice(ch.device('cuda:0'), non_blocking=True), ToTorchImage(),
+                  NormalizeImage(MEAN, STD, np.float16)],
+        'label': [IntDecoder(), ToTensor(), ToDevice('cuda:0')]})
+    for epoch in range(2):
+        order = np.random.default_rng(seed + epoch).permutation(96)
+        for b, (images, labels) in enumerate(loader):
+            assert images.shape == (32, 3, 64, 64) and images.dtype == ch.float16
+            assert images.is_contiguous(memory_format=ch.channels_last)
+            ids = order[b * 32:(b + 1) * 32]
+            want = _expected(oracle, samples, ids, seed, epoch, (64, 64), cutout=12,
+                             fill=(124, 116, 103), lut=lut)
+            got = images.permute(0, 2, 3, 1).cpu().numpy()
+            assert np.array_equal(got.view(np.uint16), want.view(np.uint16))
+            assert (labels.cpu().numpy().reshape(-1) == ids % 10).all()
+
+
+def test_flip_cutout_center_and_staged_path(tmpdir_m, oracle):
+    fn = os.path.join(tmpdir_m, 'nat_mix.beton')
+    write(fn, NaturalDS(40, hw=(90, 70), var=True, seed=8),
+          {'image': RGBImageField(write_mode='proportion', compress_probability=0.5), 'label': IntField()})
+    samples = _samples(fn)
+    assert {s[3] for s in samples} == {0, 1}
+    for cache in (True, False):
+        for cbf in (True, False):
+            ops = [CenterCropRGBImageDecoder((48, 40), 0.8)]
+            ops += [Cutout(9, (1, 2, 3)), RandomHorizontalFlip(0.5)] if cbf else \
+                [RandomHorizontalFlip(0.5), Cutout(9, (1, 2, 3))]
+            loader = Loader(fn, batch_size=8, seed=2, device_cache=cache,
+                            pipelines={'image': ops + [ToTensor(), ToDevice('cuda:0')]})
+            for b, (images, labels) in enumerate(loader):
+                ids = np.arange(b * 8, (b + 1) * 8)
+                want = _expected(oracle, samples, ids, 2, 0, (48, 40), crop='center', ratio=0.8,
+                                 cutout=9, fill=(1, 2, 3), flip_p=0.5, cut_before_flip=cbf)
+                assert np.array_equal(images.cpu().numpy(), want)
+
+
+def test_unfused_device_transforms_and_user_op(tmpdir_m, oracle):
+    """Operations the graph cannot fuse still run on the device (Cutout after
+    a Simple decoder), and a user numpy Operation gets host arrays."""
+    from dataclasses import replace
+    from ffcv_amd.pipeline.operation import Operation
+    from ffcv_amd.transforms.rng import contract_seed
+
+    class AddOne(Operation):  # reference-style host op (jit_mode numpy)
+        def generate_code(self):
+            def f(images, dst):
+                dst[:len(images)] = images + 1
+                return dst[:len(images)]
+            return f
+
+        def declare_state_and_memory(self, previous_state):
+            from ffcv_amd.pipeline.allocation_query import AllocationQuery
+            return replace(previous_state, jit_mode=True), AllocationQuery(previous_state.shape,
+                                                                           previous_state.dtype)
+    fn = os.path.join(tmpdir_m, 'const_small.beton')
+    write(fn, ConstDS(20, hw=(32, 32)), {'index': IntField(), 'value': RGBImageField()})
+    loader = Loader(fn, batch_size=4, seed=9, pipelines={
+        'value': [SimpleRGBImageDecoder(), Cutout(5, (200, 201, 202)), AddOne(), ToTensor()]})
+    for index, images in loader:
+        assert images.device.type == 'cpu'
+        for k, sid in enumerate(index.reshape(-1).tolist()):
+            rs = np.random.RandomState(contract_seed(9, 0, sid, 2))
+            y, x = rs.randint(28), rs.randint(28)
+            ref = np.full((32, 32, 3), sid % 255, np.uint8)
+            ref[y:y + 5, x:x + 5] = (200, 201, 202)
+            assert np.array_equal(images[k].numpy(), ref + 1)
+
+
+def test_corrupt_jpeg_raises(tmpdir_m):
+    fn = os.path.join(tmpdir_m, 'corrupt.beton')
+    write(fn, NaturalDS(8, hw=(40, 40)), {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    r = Reader(fn)
+    p = int(r.metadata['f0'][3]['data_ptr'])
+    with open(fn, 'r+b') as f:  # break sample 3's SOI marker
+        f.seek(p)
+        f.write(b'\x00\x00')
+    loader = Loader(fn, batch_size=4, pipelines={'image': [RandomResizedCropRGBImageDecoder((32, 32))]})
+    with pytest.raises(DecodeError, match='sample 3'):
+        for _ in loader:
+            pass
+
+
+def test_distinct_epochs_and_determinism(tmpdir_m):
+    fn = os.path.join(tmpdir_m, 'nat_det.beton')
+    write(fn, NaturalDS(16, hw=(64, 64), seed=1), {'image': RGBImageField(write_mode='jpg'),
+                                                   'label': IntField()})
+    mk = lambda: Loader(fn, batch_size=16, seed=5, pipelines={
+        'image': [RandomResizedCropRGBImageDecoder((32, 32)), ToTensor(), ToDevice('cuda:0')]})
+    a, b = mk(), mk()
+    e0a = next(iter(a))[0].cpu().clone()
+    e1a = next(iter(a))[0].cpu().clone()
+    e0b = next(iter(b))[0].cpu().clone()
+    assert ch.equal(e0a, e0b) and not ch.equal(e0a, e1a)

@@ -4,47 +4,68 @@
 // Reference: rgb_image.py:194-208 decodes every JPEG in full with
 // libjpeg-turbo (libffcv.cpp:104-106: tjDecompress2(TJPF_RGB,
 // TJFLAG_FASTDCT) = ifast IDCT + fancy upsampling + fixed-point YCbCr->RGB)
-// into a temp buffer, then crops and resizes.  Here one 256-lane workgroup
-// owns one image and runs, with workgroup barriers between phases:
+// into a temp buffer, then crops and resizes on the CPU.
 //
-//   P0  marker parse (one lane), geometry / table validation
-//   P1  Huffman lookup tables (9-bit fast LUT + canonical slow path) and the
-//       ifast dequantisation multipliers, in LDS
-//   P2  de-stuffing of the entropy-coded segment (0xFF00 -> 0xFF) into a
-//       word-aligned scratch stream (chunked count -> workgroup scan -> copy)
-//   P3  self-synchronising parallel Huffman decode: the stream is cut into
-//       one bit-range per lane; every lane decodes its range from a guessed
-//       decoder state (bit position, coefficient index z, block-in-MCU) and
-//       records the state at which it leaves the range.  The guess of lane
-//       t+1 is then replaced by lane t's exit state until no guess changes
-//       (lane 0 is exact, so after r rounds lanes 0..r are exact; JPEG
-//       streams resynchronise within a few codewords, so 1-2 extra rounds
-//       suffice in practice).  No restart markers are needed.
-//   P4  workgroup prefix scans of blocks-started and per-component DC diffs
-//       give every lane its first block index and DC predictor
-//   P5  second decode pass writes the quantised coefficients (natural order)
-//       of the blocks the crop needs into a plane-ordered scratch
-//   P6  dequantise + ifast IDCT (jidctfst.c) of exactly those blocks
-//   P7  fancy upsampling (jdsample.c) + YCbCr->RGB (jdcolor.c) of the crop ROI
-//   P8  INTER_AREA resize of the ROI (OpenCV 4.5.4) + flip/cutout/LUT
+// Two launches per batch:
 //
-// Every integer step is restated from libjpeg-turbo and matches it bit for
-// bit (tests/test_jpeg_gpu.py); the float steps of the resize are compiled
-// with -ffp-contract=off.
+// K1 jpeg_entropy_kernel -- one 256-lane workgroup per image:
+//   P0  the first 4 KB of the file are staged in LDS; one lane walks the
+//       markers there (SOF/DHT/DQT/DRI/SOS), validates geometry and tables
+//   P1  Huffman lookup tables (10-bit fast LUT + canonical slow path) and
+//       the ifast dequantisation multipliers (jddctmgr.c), in LDS
+//   P2  de-stuffing (0xFF00 -> 0xFF) of the entropy-coded segment in one
+//       read pass + workgroup scan + one write pass, into an LDS-resident
+//       word stream (images above 24 KB of entropy data use HBM scratch)
+//   P3  self-synchronising parallel Huffman decode.  The stream is cut into
+//       one bit range per lane; a lane decodes its range from a guessed state
+//       (bit position, coefficient index z, block-in-MCU), records where its
+//       blocks start, and the state at which it leaves the range.  Each
+//       further round gives lane t the exit state of lane t-1; a lane whose
+//       guess changed re-decodes only until it reaches a block start it
+//       recorded before (same bit position and MCU phase: from there its old
+//       trajectory is exact), so a round costs the resynchronisation
+//       distance, not a full range.  Lane 0 is exact, so round r fixes lanes
+//       0..r at worst; rounds end when no guess changes.
+//   P4  workgroup scan of blocks-started -> each lane's first block index
+//   P5  second decode: DC differences of every block, quantised AC
+//       coefficients (natural order) of the blocks the crop window needs
+//   P6  per-component DC prediction as a workgroup prefix scan
+//   P7  dequantise + ifast IDCT (jidctfst.c) of the window's blocks ->
+//       component planes in HBM scratch; per-image geometry record for K2
+//
+// K2 jpeg_color_resize_kernel -- one workgroup per band of 16 output rows:
+//   stages the band's source rows of the crop as RGB in LDS (jdsample.c
+//   fancy upsampling + jdcolor.c fixed-point YCbCr->RGB, once per source
+//   pixel), then computes the band's output pixels with the OpenCV 4.5.4
+//   INTER_AREA restatement + flip / cutout / LUT epilogue.  Thousands of
+//   workgroups per batch keep the CUs occupied for this latency-bound part.
+//
+// Every integer step matches libjpeg-turbo bit for bit
+// (tests/test_kernels_gpu.py); float steps use -ffp-contract=off.
 #include "api_internal.h"
 #include "device_common.h"
 
 #define JT 256
-#define FAST_BITS 9
+#define FAST_BITS 10
 #define NTAB 8
+#define HDR_BYTES 4096
+#define LDS_STREAM_BYTES 24576
+#define NEV 16
+#define BAND 16
+#define K2T 256
+#define K2_LDS 49152
 
 enum JMode { JM_RRC = 0, JM_FULL = 1, JM_COEF = 2 };
 
-struct HuffTab {
-  uint16_t lut[1 << FAST_BITS];  // (len << 8) | sym; len 0 => slow path
-  int32_t maxcode[18];
-  int32_t valoff[17];
-  uint8_t vals[256];
+// Per-image geometry written by K1 for K2.
+struct ImgInfo {
+  int32_t status;
+  int32_t W, H, ncomp, color_rgb;
+  int32_t he[3], ve[3];  // expansion factors hmax/h, vmax/v
+  int32_t cw[3], ch[3], stride[3];
+  int32_t ri, rj, rh, rw;
+  uint64_t poff[3];
+  int32_t pad[2];
 };
 
 struct JShared {
@@ -55,35 +76,40 @@ struct JShared {
   int mcux, mcuy, bpm, nblocks;
   int cw[3], ch[3], bw[3], bh[3];
   int blk_comp[10], blk_dx[10], blk_dy[10];
-  uint32_t scan_off, scan_end;
+  int ph_dc[10], ph_ac[10];  // table index per block-in-MCU
+  uint32_t scan_off;
   uint32_t dqt_off[4];
   int dqt_prec[4], dqt_ok[4];
   uint32_t dht_off[NTAB];
   int dht_ok[NTAB];
   int saw_jfif, saw_adobe, adobe_transform;
   int restart;
-  // crop window (full-res pixels) and per-component block windows
   int ri, rj, rh, rw;
   int wx0[3], wx1[3], wy0[3], wy1[3];
-  uint64_t coff[3];  // offset (in blocks) of each component in the coef scratch
-  uint64_t poff[3];  // offset (bytes) of each component plane
-  // destuff
+  uint64_t coff[3];
+  uint64_t poff[3];
   uint32_t first_marker;
   uint32_t dlen;
-  int nthr;
-  uint32_t chunk_bits;
   int any;
-  HuffTab tab[NTAB];
+  // tables
+  uint16_t lut[NTAB][1 << FAST_BITS];
+  int32_t maxcode[NTAB][18];
+  int32_t valoff[NTAB][17];
+  uint8_t vals[NTAB][256];
   int16_t qmul[3][64];
   uint8_t nat[80];
-  // per-lane decoder states
-  uint32_t g_pos[JT];
+  // lanes
   uint32_t e_pos[JT];
-  uint8_t g_z[JT], g_ph[JT], e_z[JT], e_ph[JT];
-  uint32_t cnt[JT];
-  int32_t dcs[3][JT];
+  uint16_t e_zph[JT];
   uint32_t scan_tmp[JT];
-  int32_t scan_tmp2[3][JT];
+  int32_t scan3[3][JT];
+  uint32_t ev[NEV][JT];  // block-start events: pos << 4 | phase
+  uint8_t nev[JT];
+  // header bytes, then the de-stuffed stream (same storage)
+  union {
+    uint8_t hdr[HDR_BYTES];
+    uint32_t stream[LDS_STREAM_BYTES / 4];
+  } u;
 };
 
 __constant__ uint8_t c_natural[80] = {
@@ -99,20 +125,31 @@ __constant__ int32_t c_aanscales[64] = {
     4520,  12873, 17855, 16819, 15137, 12873, 10114, 6967,  3552,  8867,  12299, 11585, 10426,
     8867,  6967,  4799,  2446,  4520,  6270,  5906,  5315,  4520,  3552,  2446,  1247};
 
-FFCV_DEV int rd16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
-
-// ----------------------------------------------------------- bit reader --
-struct BitReader {
+// ------------------------------------------------------------ bit reader --
+// The de-stuffed stream is big-endian bytes stored as 32-bit words, either in
+// LDS or (large images) in HBM scratch; reads past the end return zeros.
+struct LdsWords {
   const uint32_t *w;
   uint32_t nw;
+  FFCV_DEV uint32_t ld(uint32_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
+};
+struct GlobalWords {
+  const uint32_t *w;
+  uint32_t nw;
+  FFCV_DEV uint32_t ld(uint32_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
+};
+
+template <class Src>
+struct BitReader {
+  Src src;
   uint64_t acc;
   int nb;
   uint32_t wi;
   uint32_t pos;
-  FFCV_DEV uint32_t ld(uint32_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
-  FFCV_DEV void init(uint32_t p) {
+  FFCV_DEV void init(const Src &s, uint32_t p) {
+    src = s;
     wi = p >> 5;
-    acc = ((uint64_t)ld(wi) << 32) | (uint64_t)ld(wi + 1);
+    acc = ((uint64_t)src.ld(wi) << 32) | (uint64_t)src.ld(wi + 1);
     acc <<= (p & 31);
     nb = 64 - (int)(p & 31);
     wi += 2;
@@ -125,7 +162,7 @@ struct BitReader {
     nb -= n;
     pos += n;
     if (nb <= 32) {
-      acc |= (uint64_t)ld(wi) << (32 - nb);
+      acc |= (uint64_t)src.ld(wi) << (32 - nb);
       wi++;
       nb += 32;
     }
@@ -134,21 +171,27 @@ struct BitReader {
 
 FFCV_DEV int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(0xFFFFFFFFu << s) + 1 : x; }
 
-// Decode one Huffman symbol; returns symbol, consumes its code.
-FFCV_DEV int huff_sym(const HuffTab &t, BitReader &br) {
+struct DecState {
+  uint32_t pos;
+  int z;   // 0: next symbol is a DC; else index of the next AC coefficient
+  int ph;  // block index inside the MCU
+};
+
+// One Huffman symbol of table ti (LUT length 0 -> canonical slow path,
+// jdhuff.c jpeg_huff_decode).
+template <class Src>
+FFCV_DEV int huff_sym(const JShared &S, int ti, BitReader<Src> &br) {
   uint32_t look = br.peek16();
-  uint32_t e = t.lut[look >> (16 - FAST_BITS)];
+  uint32_t e = S.lut[ti][look >> (16 - FAST_BITS)];
   int len = (int)(e >> 8);
-  int sym;
-  if (len) {
-    sym = (int)(e & 0xff);
-  } else {
-    sym = 0;
+  int sym = (int)(e & 0xff);
+  if (len == 0) {
     len = 16;
+    sym = 0;
     for (int l = FAST_BITS + 1; l <= 16; l++) {
       int code = (int)(look >> (16 - l));
-      if (code <= t.maxcode[l]) {
-        sym = t.vals[(t.valoff[l] + code) & 0xff];
+      if (code <= S.maxcode[ti][l]) {
+        sym = S.vals[ti][(S.valoff[ti][l] + code) & 0xff];
         len = l;
         break;
       }
@@ -158,89 +201,60 @@ FFCV_DEV int huff_sym(const HuffTab &t, BitReader &br) {
   return sym;
 }
 
-struct DecState {
-  uint32_t pos;
-  int z;   // 0: next symbol is a DC; else index of next AC coefficient
-  int ph;  // block index inside the MCU
-};
-
-// Decode units (Huffman symbol + extra bits) from st until the first unit
-// boundary at or past end_bit (WRITE mode additionally stops after the last
-// block of the image).  SYNC mode counts blocks started and sums DC diffs per
-// component; WRITE mode stores coefficients of blocks inside the window.
-template <bool WRITE>
-FFCV_DEV DecState decode_range(JShared &S, const uint32_t *words, uint32_t nwords, DecState st,
-                               uint32_t end_bit, uint32_t *n_started, int32_t dcsum[3], int64_t blk,
-                               int32_t pred[3], int16_t *coef) {
-  BitReader br;
-  br.w = words;
-  br.nw = nwords;
-  br.init(st.pos);
+// SYNC decode of a lane's range [st.pos, end_bit): counts blocks started and
+// records their start events.  With old_nev >= 0 (a later round) it stops at
+// the first block start matching an event of the lane's previous trajectory
+// and splices: count and exit state come from the old run.
+template <class Src>
+FFCV_DEV DecState sync_range(JShared &S, const Src &src, DecState st, uint32_t end_bit, int lane,
+                             uint32_t *count, DecState old_exit, uint32_t old_count, int old_nev) {
+  BitReader<Src> br;
+  br.init(src, st.pos);
   int z = st.z, ph = st.ph;
+  int dco = S.ph_dc[ph], aco = S.ph_ac[ph];
   uint32_t started = 0;
-  int comp = S.blk_comp[ph];
-  const HuffTab *dct = &S.tab[S.td[comp]];
-  const HuffTab *act = &S.tab[4 + S.ta[comp]];
-  // block coordinates (WRITE mode)
-  int mx = 0, my = 0;
-  int16_t *bptr = nullptr;
-  bool inwin = false;
-  auto locate = [&](int64_t b) {
-    int64_t m = b / S.bpm;
-    int p = (int)(b - m * S.bpm);
-    my = (int)(m / S.mcux);
-    mx = (int)(m - (int64_t)my * S.mcux);
-    int c = S.blk_comp[p];
-    int bx = mx * S.hs[c] + S.blk_dx[p];
-    int by = my * S.vs[c] + S.blk_dy[p];
-    inwin = b < S.nblocks && bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c];
-    bptr = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
-  };
-  if (WRITE && z > 0) locate(blk);  // continuing a block started earlier
+  uint32_t evs[NEV];
+  int n_new = 0;
+  int j = 0;
   while (br.pos < end_bit) {
-    if (WRITE && z == 0 && blk >= S.nblocks) break;
     if (z == 0) {
-      int s = huff_sym(*dct, br);
-      int diff = 0;
-      if (s) {
-        diff = huff_extend((int)br.peek(s), s);
-        br.consume(s);
+      if (old_nev > 0) {
+        uint32_t key = (br.pos << 4) | (uint32_t)ph;
+        while (j < old_nev && S.ev[j][lane] < key) j++;
+        if (j < old_nev && S.ev[j][lane] == key) {
+          // spliced onto the previous trajectory at its j-th block start
+          int keep = min(old_nev - j, NEV - n_new);
+          if (n_new < j) {
+            for (int q = 0; q < keep; q++) S.ev[n_new + q][lane] = S.ev[j + q][lane];
+          } else if (n_new > j) {
+            for (int q = keep - 1; q >= 0; q--) S.ev[n_new + q][lane] = S.ev[j + q][lane];
+          }
+          for (int q = 0; q < n_new; q++) S.ev[q][lane] = evs[q];
+          S.nev[lane] = (uint8_t)(n_new + keep);
+          *count = started + (old_count - (uint32_t)j);
+          return old_exit;
+        }
       }
+      if (n_new < NEV) evs[n_new++] = (br.pos << 4) | (uint32_t)ph;
       started++;
-      if (WRITE) {
-        locate(blk);
-        pred[comp] += diff;
-        if (inwin) bptr[0] = (int16_t)pred[comp];
-      } else {
-        dcsum[comp] += diff;
-      }
-      z = 1;
-    } else {
-      int rs = huff_sym(*act, br);
-      int r = rs >> 4, s = rs & 15;
-      if (s) {
-        z += r;
-        int v = huff_extend((int)br.peek(s), s);
-        br.consume(s);
-        if (WRITE && inwin) bptr[S.nat[z]] = (int16_t)v;
-        z++;
-      } else if (r == 15) {
-        z += 16;
-      } else {
-        z = 64;
-      }
     }
+    int ti = z == 0 ? dco : aco;
+    int sym = huff_sym(S, ti, br);
+    int s = z == 0 ? sym : (sym & 15);
+    int r = z == 0 ? 0 : (sym >> 4);
+    br.consume(s);
+    int zac = s ? z + r + 1 : (r == 15 ? z + 16 : 64);
+    z = z == 0 ? 1 : zac;
     if (z >= 64) {
       z = 0;
-      ph++;
-      if (ph == S.bpm) ph = 0;
-      comp = S.blk_comp[ph];
-      dct = &S.tab[S.td[comp]];
-      act = &S.tab[4 + S.ta[comp]];
-      if (WRITE) blk++;
+      ph = ph + 1 == S.bpm ? 0 : ph + 1;
+      dco = S.ph_dc[ph];
+      aco = S.ph_ac[ph];
     }
   }
-  if (n_started) *n_started = started;
+  for (int q = 0; q < n_new; q++) S.ev[q][lane] = evs[q];
+  S.nev[lane] = (uint8_t)n_new;
+  *count = started;
   DecState out;
   out.pos = br.pos;
   out.z = z;
@@ -248,7 +262,64 @@ FFCV_DEV DecState decode_range(JShared &S, const uint32_t *words, uint32_t nword
   return out;
 }
 
-// Workgroup exclusive scan of one uint32 per lane (returns exclusive prefix).
+// WRITE decode: DC differences of every block and AC coefficients of the
+// blocks inside the window.  blk = index of the block in progress (z > 0) or
+// of the next block to start (z == 0).
+template <class Src>
+FFCV_DEV void write_range(JShared &S, const Src &src, DecState st, uint32_t end_bit, int64_t blk,
+                          int16_t *coef, int16_t *dcd) {
+  BitReader<Src> br;
+  br.init(src, st.pos);
+  int z = st.z, ph = st.ph;
+  int dco = S.ph_dc[ph], aco = S.ph_ac[ph];
+  const int nblocks = S.nblocks;
+  int m = (int)(blk / S.bpm);
+  int my = m / S.mcux, mx = m - my * S.mcux;
+  int16_t *bptr = coef;
+  bool inwin = false;
+  auto locate = [&]() {
+    int c = S.blk_comp[ph];
+    int bx = mx * S.hs[c] + S.blk_dx[ph];
+    int by = my * S.vs[c] + S.blk_dy[ph];
+    inwin = blk < nblocks && bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c];
+    bptr = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
+  };
+  if (z > 0) locate();
+  while (br.pos < end_bit) {
+    if (z == 0) {
+      if (blk >= nblocks) break;
+      locate();
+    }
+    int ti = z == 0 ? dco : aco;
+    int sym = huff_sym(S, ti, br);
+    int s = z == 0 ? sym : (sym & 15);
+    int r = z == 0 ? 0 : (sym >> 4);
+    int v = s ? huff_extend((int)br.peek(s), s) : 0;
+    br.consume(s);
+    if (z == 0) {
+      dcd[blk] = (int16_t)v;
+    } else if (s && inwin) {
+      bptr[S.nat[z + r]] = (int16_t)v;
+    }
+    int zac = s ? z + r + 1 : (r == 15 ? z + 16 : 64);
+    z = z == 0 ? 1 : zac;
+    if (z >= 64) {
+      z = 0;
+      blk++;
+      ph++;
+      if (ph == S.bpm) {
+        ph = 0;
+        if (++mx == S.mcux) {
+          mx = 0;
+          my++;
+        }
+      }
+      dco = S.ph_dc[ph];
+      aco = S.ph_ac[ph];
+    }
+  }
+}
+
 FFCV_DEV uint32_t wg_exscan_u32(uint32_t v, uint32_t *tmp) {
   const int t = threadIdx.x;
   tmp[t] = v;
@@ -263,19 +334,23 @@ FFCV_DEV uint32_t wg_exscan_u32(uint32_t v, uint32_t *tmp) {
   __syncthreads();
   return incl - v;
 }
-FFCV_DEV int32_t wg_exscan_i32(int32_t v, int32_t *tmp) {
+
+FFCV_DEV void wg_exscan3(int32_t v[3], int32_t (*tmp)[JT]) {
   const int t = threadIdx.x;
-  tmp[t] = v;
+  for (int c = 0; c < 3; c++) tmp[c][t] = v[c];
   __syncthreads();
   for (int off = 1; off < JT; off <<= 1) {
-    int32_t x = t >= off ? tmp[t - off] : 0;
+    int32_t x0 = t >= off ? tmp[0][t - off] : 0;
+    int32_t x1 = t >= off ? tmp[1][t - off] : 0;
+    int32_t x2 = t >= off ? tmp[2][t - off] : 0;
     __syncthreads();
-    tmp[t] += x;
+    tmp[0][t] += x0;
+    tmp[1][t] += x1;
+    tmp[2][t] += x2;
     __syncthreads();
   }
-  int32_t incl = tmp[t];
+  for (int c = 0; c < 3; c++) v[c] = tmp[c][t] - v[c];
   __syncthreads();
-  return incl - v;
 }
 
 // libjpeg post-IDCT range limit: table[x & 1023] (jdmaster.c)
@@ -285,7 +360,7 @@ FFCV_DEV uint8_t idct_rl(int x) {
 }
 FFCV_DEV int fmul8(int v, int c) { return (int)(((int64_t)v * c) >> 8); }
 
-// jidctfst.c jpeg_idct_ifast on one block (coefficients already loaded).
+// jidctfst.c jpeg_idct_ifast on one block.
 FFCV_DEV void idct_ifast_block(const int16_t *in, const int16_t *q, uint8_t *out, int stride) {
   int ws[64];
 #pragma unroll
@@ -331,7 +406,7 @@ FFCV_DEV void idct_ifast_block(const int16_t *in, const int16_t *q, uint8_t *out
     if ((w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) == 0) {
       uint8_t dc = idct_rl(w[0] >> 5);
 #pragma unroll
-      for (int k = 0; k < 8; k++) o[k] = dc;
+      for (int q2 = 0; q2 < 8; q2++) o[q2] = dc;
     } else {
       int tmp10 = w[0] + w[4], tmp11 = w[0] - w[4];
       int tmp13 = w[2] + w[6], tmp12 = fmul8(w[2] - w[6], 362) - tmp13;
@@ -352,16 +427,570 @@ FFCV_DEV void idct_ifast_block(const int16_t *in, const int16_t *q, uint8_t *out
       o[4] = idct_rl((tmp3 + tmp4) >> 5);
       o[3] = idct_rl((tmp3 - tmp4) >> 5);
     }
-    uint32_t lo = o[0] | (o[1] << 8) | (o[2] << 16) | ((uint32_t)o[3] << 24);
-    uint32_t hi = o[4] | (o[5] << 8) | (o[6] << 16) | ((uint32_t)o[7] << 24);
     uint2 v;
-    v.x = lo;
-    v.y = hi;
+    v.x = o[0] | (o[1] << 8) | (o[2] << 16) | ((uint32_t)o[3] << 24);
+    v.y = o[4] | (o[5] << 8) | (o[6] << 16) | ((uint32_t)o[7] << 24);
     *(uint2 *)(out + (uint64_t)r * stride) = v;
   }
 }
 
-// jdsample.c upsampling of component c at full-resolution sample (y, x),
+struct JpegArgs {
+  const uint8_t *base;
+  const ffcv_sample *samples;
+  const int32_t *crops;
+  const int32_t *cut;
+  const uint8_t *flips;
+  ffcv_rrc_params p;
+  void *out;
+  uint64_t out_stride;
+  int32_t *status;
+  uint8_t *dstuff;
+  uint64_t dstuff_slot;
+  int16_t *coef;
+  uint64_t coef_slot;
+  uint8_t *planes;
+  uint64_t plane_slot;
+  int16_t *dcd;
+  uint64_t dcd_slot;
+  ImgInfo *info;
+  uint32_t max_h, max_w;
+  uint64_t max_blocks;
+  uint64_t *dbg;
+};
+
+// Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
+// dbg[image*16 + slot] (never read by the kernel; off when dbg == nullptr).
+#define STAMP(slot)                                                          \
+  do {                                                                       \
+    if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + (slot)] = wall_clock64();  \
+  } while (0)
+
+// P0 (one lane): marker walk over the LDS copy of the header bytes.
+FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const ffcv_sample &smp,
+                          const JpegArgs &a, int k, int MODE) {
+  auto B = [&](uint32_t p) -> int { return p < HDR_BYTES ? S.u.hdr[p] : src[p]; };
+  auto R16 = [&](uint32_t p) -> int { return (B(p) << 8) | B(p + 1); };
+  for (int i = 0; i < 4; i++) S.dqt_ok[i] = 0;
+  for (int i = 0; i < NTAB; i++) S.dht_ok[i] = 0;
+  S.saw_jfif = S.saw_adobe = 0;
+  S.adobe_transform = 1;
+  S.restart = 0;
+  S.ncomp = 0;
+  int have_sof = 0, have_sos = 0;
+  if (nbytes < 4 || B(0) != 0xFF || B(1) != 0xD8) return FFCV_SAMPLE_BAD_MARKER;
+  uint32_t p = 2;
+  while (!have_sos) {
+    if (p + 4 > nbytes || B(p) != 0xFF) return FFCV_SAMPLE_BAD_MARKER;
+    while (p < nbytes && B(p) == 0xFF) p++;
+    if (p >= nbytes) return FFCV_SAMPLE_BAD_MARKER;
+    int m = B(p++);
+    if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+    if (m == 0xD9 || p + 2 > nbytes) return FFCV_SAMPLE_BAD_MARKER;
+    int len = R16(p);
+    if (len < 2 || p + (uint32_t)len > nbytes) return FFCV_SAMPLE_BAD_MARKER;
+    uint32_t s = p + 2;
+    int sl = len - 2;
+    if (m == 0xDB) {
+      int o = 0;
+      while (o < sl) {
+        int pq = B(s + o) >> 4, tq = B(s + o) & 15;
+        if (tq > 3) return FFCV_SAMPLE_BAD_MARKER;
+        S.dqt_off[tq] = s + o + 1;
+        S.dqt_prec[tq] = pq;
+        S.dqt_ok[tq] = 1;
+        o += 1 + (pq ? 128 : 64);
+      }
+    } else if (m == 0xC4) {
+      int o = 0;
+      while (o < sl) {
+        int tc = B(s + o) >> 4, th = B(s + o) & 15;
+        if (th > 3 || tc > 1) return FFCV_SAMPLE_BAD_MARKER;
+        int total = 0;
+        for (int l = 0; l < 16; l++) total += B(s + o + 1 + l);
+        if (total > 256) return FFCV_SAMPLE_BAD_MARKER;
+        S.dht_off[tc * 4 + th] = s + o + 1;
+        S.dht_ok[tc * 4 + th] = 1;
+        o += 17 + total;
+      }
+    } else if (m == 0xC0 || m == 0xC1) {
+      if (B(s) != 8) return FFCV_SAMPLE_UNSUPPORTED;
+      S.H = R16(s + 1);
+      S.W = R16(s + 3);
+      S.ncomp = B(s + 5);
+      if (S.ncomp != 1 && S.ncomp != 3) return FFCV_SAMPLE_UNSUPPORTED;
+      S.hmax = S.vmax = 1;
+      for (int c = 0; c < S.ncomp; c++) {
+        S.cid[c] = B(s + 6 + 3 * c);
+        S.hs[c] = B(s + 7 + 3 * c) >> 4;
+        S.vs[c] = B(s + 7 + 3 * c) & 15;
+        S.tq[c] = B(s + 8 + 3 * c) & 3;
+        if (S.hs[c] < 1 || S.hs[c] > 4 || S.vs[c] < 1 || S.vs[c] > 4) return FFCV_SAMPLE_UNSUPPORTED;
+        S.hmax = max(S.hmax, S.hs[c]);
+        S.vmax = max(S.vmax, S.vs[c]);
+      }
+      have_sof = 1;
+    } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      return FFCV_SAMPLE_UNSUPPORTED;  // progressive / lossless / arithmetic
+    } else if (m == 0xDD) {
+      S.restart = R16(s);
+    } else if (m == 0xE0) {
+      if (sl >= 5 && B(s) == 'J' && B(s + 1) == 'F' && B(s + 2) == 'I' && B(s + 3) == 'F' && B(s + 4) == 0)
+        S.saw_jfif = 1;
+    } else if (m == 0xEE) {
+      if (sl >= 12 && B(s) == 'A' && B(s + 1) == 'd' && B(s + 2) == 'o' && B(s + 3) == 'b' && B(s + 4) == 'e') {
+        S.saw_adobe = 1;
+        S.adobe_transform = B(s + 11);
+      }
+    } else if (m == 0xDA) {
+      if (!have_sof) return FFCV_SAMPLE_BAD_MARKER;
+      int ns = B(s);
+      if (ns != S.ncomp) return FFCV_SAMPLE_UNSUPPORTED;  // multi-scan sequential
+      int order[3];
+      for (int i = 0; i < ns; i++) {
+        int c = -1;
+        for (int q = 0; q < S.ncomp; q++)
+          if (S.cid[q] == B(s + 1 + 2 * i)) c = q;
+        if (c < 0) return FFCV_SAMPLE_BAD_MARKER;
+        order[i] = c;
+        S.td[c] = B(s + 2 + 2 * i) >> 4;
+        S.ta[c] = B(s + 2 + 2 * i) & 15;
+        if (S.td[c] > 3 || S.ta[c] > 3) return FFCV_SAMPLE_BAD_MARKER;
+      }
+      int nb = 0;
+      if (S.ncomp == 1) {
+        S.blk_comp[0] = order[0];
+        S.blk_dx[0] = S.blk_dy[0] = 0;
+        nb = 1;
+      } else {
+        for (int i = 0; i < ns; i++) {
+          int c = order[i];
+          for (int yy = 0; yy < S.vs[c]; yy++)
+            for (int xx = 0; xx < S.hs[c]; xx++) {
+              if (nb < 10) {
+                S.blk_comp[nb] = c;
+                S.blk_dx[nb] = xx;
+                S.blk_dy[nb] = yy;
+              }
+              nb++;
+            }
+        }
+      }
+      if (nb > 10) return FFCV_SAMPLE_UNSUPPORTED;
+      S.bpm = nb;
+      for (int b = 0; b < nb; b++) {
+        S.ph_dc[b] = S.td[S.blk_comp[b]];
+        S.ph_ac[b] = 4 + S.ta[S.blk_comp[b]];
+      }
+      S.scan_off = p + (uint32_t)len;
+      have_sos = 1;
+    }
+    p += (uint32_t)len;
+  }
+  if (S.restart) return FFCV_SAMPLE_UNSUPPORTED;
+  if (S.W != (int)smp.width || S.H != (int)smp.height) return FFCV_SAMPLE_GEOMETRY;
+  if ((uint32_t)S.W > a.max_w || (uint32_t)S.H > a.max_h) return FFCV_SAMPLE_TOO_LARGE;
+  for (int c = 0; c < S.ncomp; c++) {
+    if (!S.dqt_ok[S.tq[c]] || !S.dht_ok[S.td[c]] || !S.dht_ok[4 + S.ta[c]]) return FFCV_SAMPLE_BAD_MARKER;
+    if (S.hmax % S.hs[c] || S.vmax % S.vs[c]) return FFCV_SAMPLE_UNSUPPORTED;
+  }
+  if (S.ncomp == 3) {  // jdapimin.c default_decompress_parms colour-space rule
+    if (S.saw_jfif)
+      S.color_rgb = 0;
+    else if (S.saw_adobe)
+      S.color_rgb = S.adobe_transform == 0;
+    else
+      S.color_rgb = S.cid[0] == 82 && S.cid[1] == 71 && S.cid[2] == 66;
+  } else {
+    S.color_rgb = 0;
+  }
+  uint64_t off_blocks = 0, off_plane = 0;
+  if (S.ncomp == 1) {
+    S.cw[0] = (S.W * S.hs[0] + S.hmax - 1) / S.hmax;
+    S.ch[0] = (S.H * S.vs[0] + S.vmax - 1) / S.vmax;
+    S.mcux = (S.cw[0] + 7) / 8;
+    S.mcuy = (S.ch[0] + 7) / 8;
+    S.bw[0] = S.mcux;
+    S.bh[0] = S.mcuy;
+    S.hs[0] = S.vs[0] = 1;  // non-interleaved scan: one block per MCU
+    S.hmax = S.vmax = 1;
+  } else {
+    S.mcux = (S.W + 8 * S.hmax - 1) / (8 * S.hmax);
+    S.mcuy = (S.H + 8 * S.vmax - 1) / (8 * S.vmax);
+    for (int c = 0; c < S.ncomp; c++) {
+      S.cw[c] = (S.W * S.hs[c] + S.hmax - 1) / S.hmax;
+      S.ch[c] = (S.H * S.vs[c] + S.vmax - 1) / S.vmax;
+      S.bw[c] = S.mcux * S.hs[c];
+      S.bh[c] = S.mcuy * S.vs[c];
+    }
+  }
+  for (int c = 0; c < S.ncomp; c++) {
+    S.coff[c] = off_blocks;
+    S.poff[c] = off_plane;
+    off_blocks += (uint64_t)S.bw[c] * S.bh[c];
+    off_plane += (uint64_t)S.bw[c] * S.bh[c] * 64;
+  }
+  S.nblocks = S.mcux * S.mcuy * S.bpm;
+  if (off_blocks * 64 > a.coef_slot || off_plane > a.plane_slot || (uint64_t)S.nblocks > a.dcd_slot)
+    return FFCV_SAMPLE_TOO_LARGE;
+  if (MODE == JM_COEF && (uint64_t)S.nblocks > a.max_blocks) return FFCV_SAMPLE_TOO_LARGE;
+  if (MODE == JM_RRC) {
+    S.ri = a.crops[4 * k];
+    S.rj = a.crops[4 * k + 1];
+    S.rh = a.crops[4 * k + 2];
+    S.rw = a.crops[4 * k + 3];
+    if (S.rh <= 0 || S.rw <= 0 || S.ri < 0 || S.rj < 0 || S.ri + S.rh > S.H || S.rj + S.rw > S.W)
+      return FFCV_SAMPLE_GEOMETRY;
+  } else {
+    S.ri = 0;
+    S.rj = 0;
+    S.rh = S.H;
+    S.rw = S.W;
+  }
+  for (int c = 0; c < S.ncomp; c++) {  // blocks the crop reads (+1 sample of fancy context)
+    int he = S.hmax / S.hs[c], ve = S.vmax / S.vs[c];
+    int y0 = S.ri / ve - (ve == 2 ? 1 : 0), y1 = (S.ri + S.rh - 1) / ve + (ve == 2 ? 1 : 0);
+    int x0 = S.rj / he - (he == 2 ? 1 : 0), x1 = (S.rj + S.rw - 1) / he + (he == 2 ? 1 : 0);
+    y0 = max(y0, 0);
+    x0 = max(x0, 0);
+    y1 = min(y1, S.ch[c] - 1);
+    x1 = min(x1, S.cw[c] - 1);
+    if (MODE == JM_COEF) {
+      y0 = x0 = 0;
+      y1 = S.bh[c] * 8 - 1;
+      x1 = S.bw[c] * 8 - 1;
+    }
+    S.wy0[c] = y0 >> 3;
+    S.wy1[c] = y1 >> 3;
+    S.wx0[c] = x0 >> 3;
+    S.wx1[c] = x1 >> 3;
+  }
+  return FFCV_SAMPLE_OK;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
+  __shared__ JShared S;
+  const int t = threadIdx.x;
+  const int k = blockIdx.x;
+  const ffcv_sample smp = a.samples[k];
+  ImgInfo *info = a.info + k;
+  if (smp.mode != 0) {  // raw samples are handled by rrc_raw_kernel / gather
+    if (t == 0) {
+      a.status[k] = FFCV_SAMPLE_OK;
+      info->status = -1;  // K2 skips
+    }
+    return;
+  }
+  const uint8_t *src = a.base + smp.offset;
+  const uint32_t nbytes = (uint32_t)smp.size;
+
+  // ------------------------------------------------------------- P0 ----
+  STAMP(0);
+  for (uint32_t i = t; i < HDR_BYTES; i += JT) S.u.hdr[i] = i < nbytes ? src[i] : 0;
+  __syncthreads();
+  if (t == 0) {
+    S.status = parse_header(S, src, nbytes, smp, a, k, MODE);
+    S.first_marker = 0xFFFFFFFFu;
+    S.any = 0;
+  }
+  __syncthreads();
+  if (S.status != FFCV_SAMPLE_OK) {
+    if (t == 0) {
+      a.status[k] = S.status;
+      info->status = S.status;
+    }
+    if (MODE == JM_FULL) {  // zero-fill (K2 does it for RRC)
+      uint64_t bytes = (uint64_t)smp.height * smp.width * 3;
+      uint8_t *o = (uint8_t *)a.out + a.out_stride * k;
+      for (uint64_t i = t; i < bytes && i < a.out_stride; i += JT) o[i] = 0;
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------- P1 ----
+  STAMP(1);
+  auto HB = [&](uint32_t p) -> int { return p < HDR_BYTES ? S.u.hdr[p] : src[p]; };
+  if (t < NTAB && S.dht_ok[t]) {
+    uint32_t d = S.dht_off[t];
+    int code = 0, kk = 0;
+    for (int l = 1; l <= 16; l++) {
+      int nl = HB(d + l - 1);
+      if (nl) {
+        S.valoff[t][l] = kk - code;
+        code += nl;
+        kk += nl;
+        S.maxcode[t][l] = code - 1;
+      } else {
+        S.maxcode[t][l] = -1;
+        S.valoff[t][l] = 0;
+      }
+      code <<= 1;
+    }
+    S.maxcode[t][17] = 0x7fffffff;
+    for (int i = 0; i < kk; i++) S.vals[t][i] = (uint8_t)HB(d + 16 + i);
+  }
+  if (t < 80) S.nat[t] = c_natural[t];
+  for (int i = t; i < S.ncomp * 64; i += JT) {
+    int c = i >> 6, zz = i & 63;
+    int tq = S.tq[c];
+    uint32_t q = S.dqt_off[tq];
+    int qv = S.dqt_prec[tq] ? ((HB(q + 2 * zz) << 8) | HB(q + 2 * zz + 1)) : HB(q + zz);
+    int n = c_natural[zz];
+    S.qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
+  }
+  __syncthreads();
+  for (int i = t; i < NTAB * (1 << FAST_BITS); i += JT) {
+    int ti = i >> FAST_BITS, v = i & ((1 << FAST_BITS) - 1);
+    if (!S.dht_ok[ti]) continue;
+    uint16_t e = 0;
+    for (int l = 1; l <= FAST_BITS; l++) {
+      int code = v >> (FAST_BITS - l);
+      if (code <= S.maxcode[ti][l]) {
+        e = (uint16_t)((l << 8) | S.vals[ti][(S.valoff[ti][l] + code) & 0xff]);
+        break;
+      }
+    }
+    S.lut[ti][v] = e;
+  }
+  // zero the coefficient blocks of the window (P5 writes only nonzeros)
+  int16_t *coef = a.coef + a.coef_slot * k;
+  for (int c = 0; c < S.ncomp; c++) {
+    int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
+    int n16 = wbw * wbh * 8;
+    for (int i = t; i < n16; i += JT) {
+      int blk = i >> 3, piece = i & 7;
+      int by = S.wy0[c] + blk / wbw, bx = S.wx0[c] + blk % wbw;
+      *(uint4 *)(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64 + piece * 8) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();  // header bytes are dead from here (the stream reuses them)
+
+  // ------------------------------------------------------------- P2 ----
+  STAMP(2);
+  const uint32_t seg0 = S.scan_off;
+  const uint32_t seglen = nbytes > seg0 ? nbytes - seg0 : 0;
+  const uint32_t per = (seglen + JT - 1) / JT;
+  const uint32_t c0 = seg0 + min(seglen, per * t), c1 = seg0 + min(seglen, per * (t + 1));
+  uint32_t keep_all = 0, keep_before = 0, fm = 0xFFFFFFFFu;
+  {
+    int prev = c0 > seg0 ? src[c0 - 1] : 0;
+    for (uint32_t q = c0; q < c1; q++) {
+      int b = src[q];
+      if (b == 0xFF && fm == 0xFFFFFFFFu) {
+        int nx = q + 1 < nbytes ? src[q + 1] : 0xD9;
+        if (nx != 0x00) {
+          fm = q;
+          keep_before = keep_all;
+        }
+      }
+      keep_all += !(b == 0x00 && prev == 0xFF && q > seg0);
+      prev = b;
+    }
+    if (fm != 0xFFFFFFFFu) atomicMin(&S.first_marker, fm);
+  }
+  __syncthreads();
+  const uint32_t seg_end = S.first_marker == 0xFFFFFFFFu ? nbytes : S.first_marker;
+  uint32_t keep = c1 <= seg_end ? keep_all : (c0 >= seg_end ? 0u : keep_before);
+  uint32_t wpos = wg_exscan_u32(keep, S.scan_tmp);
+  if (t == JT - 1) S.dlen = wpos + keep;
+  __syncthreads();
+  const uint32_t dlen = S.dlen;
+  const bool in_lds = dlen + 16 <= LDS_STREAM_BYTES;
+  uint8_t *gds = a.dstuff + a.dstuff_slot * k;
+  uint8_t *dsb = in_lds ? (uint8_t *)S.u.stream : gds;
+  {
+    uint32_t end = min(c1, seg_end);
+    int prev = c0 > seg0 ? src[c0 - 1] : 0;
+    for (uint32_t q = c0; q < end; q++) {
+      int b = src[q];
+      if (!(b == 0x00 && prev == 0xFF && q > seg0)) dsb[wpos++] = (uint8_t)b;
+      prev = b;
+    }
+  }
+  __syncthreads();
+  if (t < 16) dsb[dlen + t] = 0;  // zero fill, as libjpeg past a marker
+  __syncthreads();
+  const uint32_t nwords = (dlen + 3) / 4;
+  const uint32_t total_bits = dlen * 8;
+
+  // ------------------------------------------------------------- P3 ----
+  STAMP(3);
+  uint32_t nthr = (total_bits + 191) / 192;
+  nthr = max(1u, min(nthr, (uint32_t)JT));
+  const uint32_t cbits = (total_bits + nthr - 1) / nthr;
+  const bool active = t < (int)nthr;
+  const uint32_t my_end = active ? (t == (int)nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
+  DecState g;
+  g.pos = active ? t * cbits : 0;
+  g.z = 0;
+  g.ph = 0;
+  uint32_t my_cnt = 0;
+  DecState e = g;
+  S.nev[t] = 0;
+  LdsWords lw{S.u.stream, nwords};
+  GlobalWords gw{(const uint32_t *)gds, nwords};
+  if (active) {
+    if (in_lds)
+      e = sync_range(S, lw, g, my_end, t, &my_cnt, g, 0, -1);
+    else
+      e = sync_range(S, gw, g, my_end, t, &my_cnt, g, 0, -1);
+  }
+  int rounds = 0;
+  for (;;) {
+    S.e_pos[t] = e.pos;
+    S.e_zph[t] = (uint16_t)(e.z | (e.ph << 8));
+    __syncthreads();
+    bool changed = false;
+    DecState ng = g;
+    if (active && t > 0) {
+      ng.pos = S.e_pos[t - 1];
+      ng.z = S.e_zph[t - 1] & 0xff;
+      ng.ph = S.e_zph[t - 1] >> 8;
+      changed = ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph;
+    }
+    int anyc = __syncthreads_or(changed);
+    if (!anyc) break;
+    rounds++;
+    if (changed) {
+      g = ng;
+      if (g.pos >= my_end) {
+        e = g;
+        my_cnt = 0;
+        S.nev[t] = 0;
+      } else {
+        int onev = S.nev[t];
+        uint32_t ocnt = my_cnt;
+        if (in_lds)
+          e = sync_range(S, lw, g, my_end, t, &my_cnt, e, ocnt, onev);
+        else
+          e = sync_range(S, gw, g, my_end, t, &my_cnt, e, ocnt, onev);
+      }
+    }
+  }
+  if (!active) my_cnt = 0;
+  if (a.dbg && t == 0) {
+    a.dbg[(uint64_t)k * 16 + 12] = (uint64_t)rounds;
+    a.dbg[(uint64_t)k * 16 + 13] = (uint64_t)nthr;
+  }
+
+  // ------------------------------------------------------------- P4 ----
+  STAMP(4);
+  const uint32_t blk_base = wg_exscan_u32(my_cnt, S.scan_tmp);
+  if (active) {
+    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
+    if (cur < 0 || (cur % S.bpm) != g.ph) S.any = 1;  // inconsistent stream
+  }
+
+  // ------------------------------------------------------------- P5 ----
+  STAMP(5);
+  int16_t *dcd = a.dcd + a.dcd_slot * k;
+  if (active && g.pos < my_end) {
+    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
+    if (cur >= 0) {
+      if (in_lds)
+        write_range(S, lw, g, my_end, cur, coef, dcd);
+      else
+        write_range(S, gw, g, my_end, cur, coef, dcd);
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------- P6 ----
+  // DC prediction (jdhuff.c last_dc_val): per-component running sum of DC
+  // differences in MCU block order, as a workgroup scan over block ranges.
+  STAMP(6);
+  {
+    const int nb = S.nblocks;
+    const int per_b = (nb + JT - 1) / JT;
+    const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
+    int32_t sum[3] = {0, 0, 0};
+    int ph = b0 % S.bpm;
+    for (int b = b0; b < b1; b++) {
+      sum[S.blk_comp[ph]] += dcd[b];
+      if (++ph == S.bpm) ph = 0;
+    }
+    int32_t pred[3] = {sum[0], sum[1], sum[2]};
+    wg_exscan3(pred, S.scan3);
+    ph = b0 % S.bpm;
+    int m = b0 / S.bpm;
+    int my = m / S.mcux, mx = m - my * S.mcux;
+    for (int b = b0; b < b1; b++) {
+      int c = S.blk_comp[ph];
+      pred[c] += dcd[b];
+      int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
+      if (bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c])
+        coef[(S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64] = (int16_t)pred[c];
+      if (++ph == S.bpm) {
+        ph = 0;
+        if (++mx == S.mcux) {
+          mx = 0;
+          my++;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  if (MODE == JM_COEF) {
+    int16_t *o = (int16_t *)a.out + a.out_stride / 2 * k;
+    for (int64_t b = t; b < S.nblocks; b += JT) {
+      int64_t m = b / S.bpm;
+      int ph = (int)(b - m * S.bpm);
+      int my = (int)(m / S.mcux), mx = (int)(m - (int64_t)my * S.mcux);
+      int c = S.blk_comp[ph];
+      int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
+      const uint4 *sp = (const uint4 *)(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64);
+      uint4 *dp = (uint4 *)(o + b * 64);
+      for (int i = 0; i < 8; i++) dp[i] = sp[i];
+    }
+    if (t == 0) a.status[k] = S.any ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
+    return;
+  }
+
+  // ------------------------------------------------------------- P7 ----
+  STAMP(7);
+  uint8_t *planes = a.planes + a.plane_slot * k;
+  for (int c = 0; c < S.ncomp; c++) {
+    int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
+    int stride = S.bw[c] * 8;
+    for (int i = t; i < wbw * wbh; i += JT) {
+      int by = S.wy0[c] + i / wbw, bx = S.wx0[c] + i % wbw;
+      const int16_t *cp = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
+      int16_t blk[64];
+#pragma unroll
+      for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(blk + p8 * 8) = ((const uint4 *)cp)[p8];
+      idct_ifast_block(blk, S.qmul[c], planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
+    }
+  }
+  if (t == 0) {
+    info->status = FFCV_SAMPLE_OK;
+    info->W = S.W;
+    info->H = S.H;
+    info->ncomp = S.ncomp;
+    info->color_rgb = S.color_rgb;
+    for (int c = 0; c < 3; c++) {
+      bool v = c < S.ncomp;
+      info->he[c] = v ? S.hmax / S.hs[c] : 1;
+      info->ve[c] = v ? S.vmax / S.vs[c] : 1;
+      info->cw[c] = v ? S.cw[c] : 0;
+      info->ch[c] = v ? S.ch[c] : 0;
+      info->stride[c] = v ? S.bw[c] * 8 : 0;
+      info->poff[c] = v ? S.poff[c] : 0;
+    }
+    info->ri = S.ri;
+    info->rj = S.rj;
+    info->rh = S.rh;
+    info->rw = S.rw;
+    a.status[k] = S.any ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
+  }
+  STAMP(8);
+}
+
+// ======================================================================= //
+// K2: fancy upsampling + colour conversion into LDS, INTER_AREA + epilogue //
+// ======================================================================= //
+
+// jdsample.c upsampling of one component at full-resolution sample (y, x),
 // with libjpeg's context-row edge replication.
 FFCV_DEV int plane_at(const uint8_t *p, int stride, int ch, int y, int x) {
   y = y < 0 ? 0 : (y >= ch ? ch - 1 : y);
@@ -404,598 +1033,124 @@ FFCV_DEV int upsample_at(const uint8_t *p, int stride, int cw, int ch, int he, i
   return p[(uint64_t)(y / ve) * stride + x / he];  // int_upsample
 }
 
-// jdcolor.c ycc_rgb_convert with build_ycc_rgb_table's fixed point (16 bits)
+// jdcolor.c ycc_rgb_convert with build_ycc_rgb_table's fixed point
 FFCV_DEV void ycc_rgb(int y, int cb, int cr, int out[3]) {
   int x_cb = cb - 128, x_cr = cr - 128;
-  int r = y + ((91881 * x_cr + 32768) >> 16);
-  int g = y + ((-22554 * x_cb + 32768 + -46802 * x_cr) >> 16);
-  int b = y + ((116130 * x_cb + 32768) >> 16);
-  out[0] = sat_u8i(r);
-  out[1] = sat_u8i(g);
-  out[2] = sat_u8i(b);
+  out[0] = sat_u8i(y + ((91881 * x_cr + 32768) >> 16));
+  out[1] = sat_u8i(y + ((-22554 * x_cb + 32768 + -46802 * x_cr) >> 16));
+  out[2] = sat_u8i(y + ((116130 * x_cb + 32768) >> 16));
 }
 
-struct JpegArgs {
-  const uint8_t *base;
-  const ffcv_sample *samples;
-  const int32_t *crops;
-  const int32_t *cut;
-  const uint8_t *flips;
-  ffcv_rrc_params p;
-  void *out;
-  uint64_t out_stride;
-  int32_t *status;
-  // scratch
-  uint8_t *dstuff;
-  uint64_t dstuff_slot;
-  int16_t *coef;
-  uint64_t coef_slot;  // in int16 elements
-  uint8_t *planes;
-  uint64_t plane_slot;
-  uint8_t *roi;
-  uint64_t roi_slot;
-  uint32_t max_h, max_w;
-  uint64_t max_blocks;  // JM_COEF output capacity
-  uint64_t *dbg;        // optional per-image phase stamps (diagnostic builds)
-};
+FFCV_DEV void pixel_rgb(const ImgInfo &I, const uint8_t *planes, int Y, int X, int v[3]) {
+  if (I.ncomp == 1) {
+    int g = planes[I.poff[0] + (uint64_t)Y * I.stride[0] + X];
+    v[0] = v[1] = v[2] = g;
+    return;
+  }
+  int s0 = upsample_at(planes + I.poff[0], I.stride[0], I.cw[0], I.ch[0], I.he[0], I.ve[0], Y, X);
+  int s1 = upsample_at(planes + I.poff[1], I.stride[1], I.cw[1], I.ch[1], I.he[1], I.ve[1], Y, X);
+  int s2 = upsample_at(planes + I.poff[2], I.stride[2], I.cw[2], I.ch[2], I.he[2], I.ve[2], Y, X);
+  if (I.color_rgb) {
+    v[0] = s0;
+    v[1] = s1;
+    v[2] = s2;
+  } else {
+    ycc_rgb(s0, s1, s2, v);
+  }
+}
 
-// Diagnostic stamps: lane 0 records s_memtime at phase boundaries into
-// dbg[image*16 + slot] (never read by the kernel; off when dbg == nullptr).
-#define STAMP(slot)                                                          \
-  do {                                                                       \
-    if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + (slot)] = wall_clock64();  \
-  } while (0)
-
-struct RoiScratch {
+struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
   const uint8_t *p;
-  uint64_t step;
-  FFCV_DEV int at(int y, int x, int c) const { return p[(uint64_t)y * step + (uint64_t)x * 3 + c]; }
+  int row0;
+  int step;
+  FFCV_DEV int at(int y, int x, int c) const { return p[(y - row0) * step + x * 3 + c]; }
 };
+
+// Source rows of the crop that output rows [oy0, oy1) read.
+FFCV_DEV void band_rows(const ResizePlan &P, int oy0, int oy1, int *r0, int *r1) {
+  if (P.kind == 0) {
+    *r0 = oy0;
+    *r1 = oy1 - 1;
+  } else if (P.kind == 1) {
+    *r0 = oy0 * P.isy;
+    *r1 = oy1 * P.isy - 1;
+  } else if (P.kind == 2) {
+    AreaTaps a = area_taps(P.sh, P.scale_y, oy0);
+    AreaTaps b = area_taps(P.sh, P.scale_y, oy1 - 1);
+    *r0 = a.lo;
+    *r1 = b.hi;
+  } else {
+    int s0 = (int)floor(oy0 * P.scale_y), s1 = (int)floor((oy1 - 1) * P.scale_y) + 1;
+    *r0 = s0;
+    *r1 = s1;
+  }
+  *r0 = min(max(*r0, 0), P.sh - 1);
+  *r1 = min(max(*r1, 0), P.sh - 1);
+}
 
 template <int MODE, bool FP16>
-__global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
-  __shared__ JShared S;
+__global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint16_t *s_lut = (uint16_t *)lds;  // 768 entries (FP16)
+  uint8_t *roi = lds + (FP16 ? 1536 : 0);
   const int t = threadIdx.x;
-  const int k = blockIdx.x;
-  const ffcv_sample smp = a.samples[k];
-  if (smp.mode != 0) {  // raw samples are handled by rrc_raw_kernel / gather
-    if (t == 0) a.status[k] = FFCV_SAMPLE_OK;
-    return;
-  }
-  const uint8_t *src = a.base + smp.offset;
-  const uint32_t nbytes = (uint32_t)smp.size;
-
-  // ------------------------------------------------------------- P0 ----
-  STAMP(0);
-  if (t == 0) {
-    int st = FFCV_SAMPLE_OK;
-    for (int i = 0; i < 4; i++) S.dqt_ok[i] = 0;
-    for (int i = 0; i < NTAB; i++) S.dht_ok[i] = 0;
-    S.saw_jfif = S.saw_adobe = 0;
-    S.adobe_transform = 1;
-    S.restart = 0;
-    S.ncomp = 0;
-    int have_sof = 0, have_sos = 0;
-    if (nbytes < 4 || src[0] != 0xFF || src[1] != 0xD8) st = FFCV_SAMPLE_BAD_MARKER;
-    uint32_t p = 2;
-    while (st == FFCV_SAMPLE_OK && !have_sos) {
-      if (p + 4 > nbytes || src[p] != 0xFF) {
-        st = FFCV_SAMPLE_BAD_MARKER;
-        break;
-      }
-      while (p < nbytes && src[p] == 0xFF) p++;
-      if (p >= nbytes) {
-        st = FFCV_SAMPLE_BAD_MARKER;
-        break;
-      }
-      int m = src[p++];
-      if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
-      if (m == 0xD9 || p + 2 > nbytes) {
-        st = FFCV_SAMPLE_BAD_MARKER;
-        break;
-      }
-      int len = rd16(src + p);
-      if (len < 2 || p + (uint32_t)len > nbytes) {
-        st = FFCV_SAMPLE_BAD_MARKER;
-        break;
-      }
-      const uint8_t *s = src + p + 2;
-      int sl = len - 2;
-      if (m == 0xDB) {
-        int o = 0;
-        while (o < sl) {
-          int pq = s[o] >> 4, tq = s[o] & 15;
-          if (tq > 3) {
-            st = FFCV_SAMPLE_BAD_MARKER;
-            break;
-          }
-          S.dqt_off[tq] = p + 2 + o + 1;
-          S.dqt_prec[tq] = pq;
-          S.dqt_ok[tq] = 1;
-          o += 1 + (pq ? 128 : 64);
-        }
-      } else if (m == 0xC4) {
-        int o = 0;
-        while (o < sl) {
-          int tc = s[o] >> 4, th = s[o] & 15;
-          if (th > 3 || tc > 1) {
-            st = FFCV_SAMPLE_BAD_MARKER;
-            break;
-          }
-          int total = 0;
-          for (int l = 0; l < 16; l++) total += s[o + 1 + l];
-          if (total > 256) {
-            st = FFCV_SAMPLE_BAD_MARKER;
-            break;
-          }
-          S.dht_off[tc * 4 + th] = p + 2 + o + 1;
-          S.dht_ok[tc * 4 + th] = 1;
-          o += 17 + total;
-        }
-      } else if (m == 0xC0 || m == 0xC1) {
-        if (s[0] != 8) {
-          st = FFCV_SAMPLE_UNSUPPORTED;
-          break;
-        }
-        S.H = rd16(s + 1);
-        S.W = rd16(s + 3);
-        S.ncomp = s[5];
-        if (S.ncomp != 1 && S.ncomp != 3) {
-          st = FFCV_SAMPLE_UNSUPPORTED;
-          break;
-        }
-        S.hmax = S.vmax = 1;
-        for (int c = 0; c < S.ncomp; c++) {
-          S.cid[c] = s[6 + 3 * c];
-          S.hs[c] = s[7 + 3 * c] >> 4;
-          S.vs[c] = s[7 + 3 * c] & 15;
-          S.tq[c] = s[8 + 3 * c] & 3;
-          if (S.hs[c] < 1 || S.hs[c] > 4 || S.vs[c] < 1 || S.vs[c] > 4) st = FFCV_SAMPLE_UNSUPPORTED;
-          S.hmax = max(S.hmax, S.hs[c]);
-          S.vmax = max(S.vmax, S.vs[c]);
-        }
-        have_sof = 1;
-      } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-        st = FFCV_SAMPLE_UNSUPPORTED;  // progressive / lossless / arithmetic
-      } else if (m == 0xDD) {
-        S.restart = rd16(s);
-      } else if (m == 0xE0) {
-        if (sl >= 5 && s[0] == 'J' && s[1] == 'F' && s[2] == 'I' && s[3] == 'F' && s[4] == 0) S.saw_jfif = 1;
-      } else if (m == 0xEE) {
-        if (sl >= 12 && s[0] == 'A' && s[1] == 'd' && s[2] == 'o' && s[3] == 'b' && s[4] == 'e') {
-          S.saw_adobe = 1;
-          S.adobe_transform = s[11];
-        }
-      } else if (m == 0xDA) {
-        if (!have_sof) {
-          st = FFCV_SAMPLE_BAD_MARKER;
-          break;
-        }
-        int ns = s[0];
-        if (ns != S.ncomp) {
-          st = FFCV_SAMPLE_UNSUPPORTED;  // multi-scan sequential
-          break;
-        }
-        int order[3];
-        for (int i = 0; i < ns; i++) {
-          int c = -1;
-          for (int q = 0; q < S.ncomp; q++)
-            if (S.cid[q] == s[1 + 2 * i]) c = q;
-          if (c < 0) {
-            st = FFCV_SAMPLE_BAD_MARKER;
-            break;
-          }
-          order[i] = c;
-          S.td[c] = s[2 + 2 * i] >> 4;
-          S.ta[c] = s[2 + 2 * i] & 15;
-          if (S.td[c] > 3 || S.ta[c] > 3) st = FFCV_SAMPLE_BAD_MARKER;
-        }
-        if (st) break;
-        // blocks of one MCU in scan order
-        int nb = 0;
-        if (S.ncomp == 1) {
-          S.blk_comp[0] = order[0];
-          S.blk_dx[0] = S.blk_dy[0] = 0;
-          nb = 1;
-        } else {
-          for (int i = 0; i < ns; i++) {
-            int c = order[i];
-            for (int yy = 0; yy < S.vs[c]; yy++)
-              for (int xx = 0; xx < S.hs[c]; xx++) {
-                if (nb < 10) {
-                  S.blk_comp[nb] = c;
-                  S.blk_dx[nb] = xx;
-                  S.blk_dy[nb] = yy;
-                }
-                nb++;
-              }
-          }
-        }
-        if (nb > 10) {
-          st = FFCV_SAMPLE_UNSUPPORTED;
-          break;
-        }
-        S.bpm = nb;
-        S.scan_off = p + (uint32_t)len;
-        have_sos = 1;
-      }
-      p += (uint32_t)len;
-    }
-    if (st == FFCV_SAMPLE_OK) {
-      if (S.restart) st = FFCV_SAMPLE_UNSUPPORTED;
-      if (S.W != (int)smp.width || S.H != (int)smp.height) st = FFCV_SAMPLE_GEOMETRY;
-      if ((uint32_t)S.W > a.max_w || (uint32_t)S.H > a.max_h) st = FFCV_SAMPLE_TOO_LARGE;
-      for (int c = 0; c < S.ncomp && st == FFCV_SAMPLE_OK; c++) {
-        if (!S.dqt_ok[S.tq[c]] || !S.dht_ok[S.td[c]] || !S.dht_ok[4 + S.ta[c]]) st = FFCV_SAMPLE_BAD_MARKER;
-        if (S.hmax % S.hs[c] || S.vmax % S.vs[c]) st = FFCV_SAMPLE_UNSUPPORTED;
-      }
-    }
-    if (st == FFCV_SAMPLE_OK) {
-      if (S.ncomp == 3) {
-        if (S.saw_jfif)
-          S.color_rgb = 0;
-        else if (S.saw_adobe)
-          S.color_rgb = S.adobe_transform == 0;
-        else
-          S.color_rgb = S.cid[0] == 82 && S.cid[1] == 71 && S.cid[2] == 66;
-      } else {
-        S.color_rgb = 0;
-      }
-      uint64_t off_blocks = 0, off_plane = 0;
-      if (S.ncomp == 1) {
-        S.cw[0] = (S.W * S.hs[0] + S.hmax - 1) / S.hmax;
-        S.ch[0] = (S.H * S.vs[0] + S.vmax - 1) / S.vmax;
-        S.mcux = (S.cw[0] + 7) / 8;
-        S.mcuy = (S.ch[0] + 7) / 8;
-        S.bw[0] = S.mcux;
-        S.bh[0] = S.mcuy;
-        S.hs[0] = S.vs[0] = 1;  // non-interleaved scan: one block per MCU
-        S.hmax = S.vmax = 1;
-      } else {
-        S.mcux = (S.W + 8 * S.hmax - 1) / (8 * S.hmax);
-        S.mcuy = (S.H + 8 * S.vmax - 1) / (8 * S.vmax);
-        for (int c = 0; c < S.ncomp; c++) {
-          S.cw[c] = (S.W * S.hs[c] + S.hmax - 1) / S.hmax;
-          S.ch[c] = (S.H * S.vs[c] + S.vmax - 1) / S.vmax;
-          S.bw[c] = S.mcux * S.hs[c];
-          S.bh[c] = S.mcuy * S.vs[c];
-        }
-      }
-      for (int c = 0; c < S.ncomp; c++) {
-        S.coff[c] = off_blocks;
-        S.poff[c] = off_plane;
-        off_blocks += (uint64_t)S.bw[c] * S.bh[c];
-        off_plane += (uint64_t)S.bw[c] * S.bh[c] * 64;
-      }
-      S.nblocks = S.mcux * S.mcuy * S.bpm;
-      if (off_blocks * 64 > a.coef_slot || off_plane > a.plane_slot) st = FFCV_SAMPLE_TOO_LARGE;
-      if (MODE == JM_COEF && (uint64_t)S.nblocks > a.max_blocks) st = FFCV_SAMPLE_TOO_LARGE;
-      // crop window in full-resolution pixels
-      if (MODE == JM_RRC) {
-        S.ri = a.crops[4 * k];
-        S.rj = a.crops[4 * k + 1];
-        S.rh = a.crops[4 * k + 2];
-        S.rw = a.crops[4 * k + 3];
-        if (S.rh <= 0 || S.rw <= 0 || S.ri < 0 || S.rj < 0 || S.ri + S.rh > S.H || S.rj + S.rw > S.W)
-          st = FFCV_SAMPLE_GEOMETRY;
-      } else {
-        S.ri = 0;
-        S.rj = 0;
-        S.rh = S.H;
-        S.rw = S.W;
-      }
-      if (MODE == JM_RRC && (uint64_t)S.rh * S.rw * 3 > a.roi_slot) st = FFCV_SAMPLE_TOO_LARGE;
-      for (int c = 0; c < S.ncomp; c++) {
-        int he = S.hmax / S.hs[c], ve = S.vmax / S.vs[c];
-        int y0 = S.ri / ve - (ve == 2 ? 1 : 0), y1 = (S.ri + S.rh - 1) / ve + (ve == 2 ? 1 : 0);
-        int x0 = S.rj / he - (he == 2 ? 1 : 0), x1 = (S.rj + S.rw - 1) / he + (he == 2 ? 1 : 0);
-        y0 = max(y0, 0);
-        x0 = max(x0, 0);
-        y1 = min(y1, S.ch[c] - 1);
-        x1 = min(x1, S.cw[c] - 1);
-        if (MODE == JM_COEF) {
-          y0 = x0 = 0;
-          y1 = S.bh[c] * 8 - 1;
-          x1 = S.bw[c] * 8 - 1;
-        }
-        S.wy0[c] = y0 >> 3;
-        S.wy1[c] = y1 >> 3;
-        S.wx0[c] = x0 >> 3;
-        S.wx1[c] = x1 >> 3;
-      }
-    }
-    S.status = st;
-    S.first_marker = 0xFFFFFFFFu;
-    S.any = 0;
-  }
-  __syncthreads();
-  if (S.status != FFCV_SAMPLE_OK) {
-    // zero-fill this sample's output and report
+  const int k = blockIdx.y;
+  const int band = blockIdx.x;
+  const ImgInfo I = a.info[k];
+  if (I.status == -1) return;  // raw sample (handled by the raw kernel)
+  const int out_h = MODE == JM_FULL ? (int)a.samples[k].height : a.p.out_h;
+  const int out_w = MODE == JM_FULL ? (int)a.samples[k].width : a.p.out_w;
+  const int oy0 = band * BAND, oy1 = min(out_h, oy0 + BAND);
+  if (oy0 >= out_h) return;
+  char *ob = (char *)a.out + a.out_stride * k;
+  const int esz = FP16 ? 2 : 1;
+  if (I.status != FFCV_SAMPLE_OK) {  // zero-fill this band
     if (MODE == JM_RRC) {
-      uint64_t bytes = (uint64_t)a.p.out_h * a.p.out_w * 3 * (FP16 ? 2 : 1);
-      uint8_t *o = (uint8_t *)a.out + a.out_stride * k;
-      for (uint64_t i = t; i < bytes; i += JT) o[i] = 0;
-    } else if (MODE == JM_FULL) {
-      uint64_t bytes = (uint64_t)smp.height * smp.width * 3;
-      uint8_t *o = (uint8_t *)a.out + a.out_stride * k;
-      for (uint64_t i = t; i < bytes && i < a.out_stride; i += JT) o[i] = 0;
+      uint64_t row = (uint64_t)out_w * 3 * esz;
+      for (uint64_t i = t; i < row * (oy1 - oy0); i += K2T) ob[row * oy0 + i] = 0;
     }
-    if (t == 0) a.status[k] = S.status;
     return;
   }
-
-  // ------------------------------------------------------------- P1 ----
-  STAMP(1);
-  if (t < NTAB) {
-    if (S.dht_ok[t]) {
-      HuffTab &T = S.tab[t];
-      const uint8_t *d = src + S.dht_off[t];
-      int code = 0, kk = 0;
-      for (int l = 1; l <= 16; l++) {
-        int nl = d[l - 1];
-        if (nl) {
-          T.valoff[l] = kk - code;
-          code += nl;
-          kk += nl;
-          T.maxcode[l] = code - 1;
-        } else {
-          T.maxcode[l] = -1;
-          T.valoff[l] = 0;
-        }
-        code <<= 1;
-      }
-      T.maxcode[17] = 0x7fffffff;
-      for (int i = 0; i < kk; i++) T.vals[i] = d[16 + i];
-    }
-  }
-  if (t < 80) S.nat[t] = c_natural[t];
-  __syncthreads();
-  for (int i = t; i < NTAB * (1 << FAST_BITS); i += JT) {
-    int ti = i >> FAST_BITS, v = i & ((1 << FAST_BITS) - 1);
-    if (!S.dht_ok[ti]) continue;
-    HuffTab &T = S.tab[ti];
-    uint16_t e = 0;
-    for (int l = 1; l <= FAST_BITS; l++) {
-      int code = v >> (FAST_BITS - l);
-      if (code <= T.maxcode[l]) {
-        e = (uint16_t)((l << 8) | T.vals[(T.valoff[l] + code) & 0xff]);
-        break;
-      }
-    }
-    T.lut[v] = e;
-  }
-  for (int i = t; i < S.ncomp * 64; i += JT) {
-    int c = i >> 6, zz = i & 63;  // zz: zigzag index in the DQT
-    int tq = S.tq[c];
-    const uint8_t *q = src + S.dqt_off[tq];
-    int qv = S.dqt_prec[tq] ? rd16(q + 2 * zz) : q[zz];
-    int n = c_natural[zz];
-    S.qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
-  }
-
-  // zero the coefficient blocks of the window (P5 writes only nonzeros)
-  int16_t *coef = a.coef + a.coef_slot * k;
-  __syncthreads();
-  for (int c = 0; c < S.ncomp; c++) {
-    int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
-    int n16 = wbw * wbh * 8;  // 16-byte pieces
-    for (int i = t; i < n16; i += JT) {
-      int blk = i >> 3, piece = i & 7;
-      int by = S.wy0[c] + blk / wbw, bx = S.wx0[c] + blk % wbw;
-      uint4 zero = make_uint4(0, 0, 0, 0);
-      *(uint4 *)(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64 + piece * 8) = zero;
-    }
-  }
-
-  // ------------------------------------------------------------- P2 ----
-  STAMP(2);
-  // entropy-coded segment: [scan_off, first marker)
-  const uint32_t seg0 = S.scan_off;
-  const uint32_t seglen = nbytes > seg0 ? nbytes - seg0 : 0;
-  const uint32_t per = (seglen + JT - 1) / JT;
-  const uint32_t c0 = seg0 + min(seglen, per * t), c1 = seg0 + min(seglen, per * (t + 1));
-  {
-    uint32_t fm = 0xFFFFFFFFu;
-    for (uint32_t q = c0; q < c1; q++) {
-      if (src[q] == 0xFF) {
-        uint8_t nx = q + 1 < nbytes ? src[q + 1] : 0xD9;
-        if (nx != 0x00) {
-          fm = q;
-          break;
-        }
-      }
-    }
-    if (fm != 0xFFFFFFFFu) atomicMin(&S.first_marker, fm);
-  }
-  __syncthreads();
-  const uint32_t seg_end = S.first_marker == 0xFFFFFFFFu ? nbytes : S.first_marker;
-  uint32_t keep = 0;
-  for (uint32_t q = c0; q < min(c1, seg_end); q++)
-    keep += !(src[q] == 0x00 && q > seg0 && src[q - 1] == 0xFF);
-  uint32_t wpos = wg_exscan_u32(keep, S.scan_tmp);
-  uint8_t *ds = a.dstuff + a.dstuff_slot * k;
-  for (uint32_t q = c0; q < min(c1, seg_end); q++) {
-    if (!(src[q] == 0x00 && q > seg0 && src[q - 1] == 0xFF)) ds[wpos++] = src[q];
-  }
-  if (t == JT - 1) {
-    S.dlen = wpos;
-    for (int i = 0; i < 16; i++) ds[wpos + i] = 0;  // zero fill, as libjpeg past a marker
-  }
-  __syncthreads();
-  const uint32_t dlen = S.dlen;
-  const uint32_t *words = (const uint32_t *)ds;
-  const uint32_t nwords = (dlen + 3) / 4;
-  const uint32_t total_bits = dlen * 8;
-
-  // ------------------------------------------------------------- P3 ----
-  STAMP(3);
-  if (t == 0) {
-    // at least ~192 bits per lane so resynchronisation is cheap relative to work
-    uint32_t nthr = (total_bits + 191) / 192;
-    nthr = max(1u, min(nthr, (uint32_t)JT));
-    uint32_t cb = (total_bits + nthr - 1) / nthr;
-    S.nthr = (int)nthr;
-    S.chunk_bits = cb;
-  }
-  __syncthreads();
-  const int nthr = S.nthr;
-  const uint32_t cbits = S.chunk_bits;
-  const bool active = t < nthr;
-  const uint32_t my_end = active ? (t == nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
-  DecState g;
-  g.pos = active ? t * cbits : 0;
-  g.z = 0;
-  g.ph = 0;
-  uint32_t my_cnt = 0;
-  int32_t my_dc[3] = {0, 0, 0};
-  DecState e = g;
-  if (active) e = decode_range<false>(S, words, nwords, g, my_end, &my_cnt, my_dc, 0, nullptr, nullptr);
-  for (int round = 0; round < JT + 1; round++) {
-    S.e_pos[t] = e.pos;
-    S.e_z[t] = (uint8_t)e.z;
-    S.e_ph[t] = (uint8_t)e.ph;
-    __syncthreads();
-    bool changed = false;
-    DecState ng = g;
-    if (active && t > 0) {
-      ng.pos = S.e_pos[t - 1];
-      ng.z = S.e_z[t - 1];
-      ng.ph = S.e_ph[t - 1];
-      changed = ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph;
-    }
-    int anyc = __syncthreads_or(changed);
-    if (!anyc) {
-      if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + 12] = (uint64_t)round;
-      break;
-    }
-    if (changed) {
-      g = ng;
-      my_dc[0] = my_dc[1] = my_dc[2] = 0;
-      if (g.pos >= my_end) {  // previous unit already crossed my whole range
-        e = g;
-        my_cnt = 0;
-      } else {
-        e = decode_range<false>(S, words, nwords, g, my_end, &my_cnt, my_dc, 0, nullptr, nullptr);
-      }
-    }
-  }
-  if (!active) {
-    my_cnt = 0;
-    my_dc[0] = my_dc[1] = my_dc[2] = 0;
-  }
-
-  // ------------------------------------------------------------- P4 ----
-  STAMP(4);
-  if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + 13] = (uint64_t)nthr;
-  const uint32_t blk_base = wg_exscan_u32(my_cnt, S.scan_tmp);
-  int32_t pred[3];
-  for (int c = 0; c < 3; c++) pred[c] = wg_exscan_i32(my_dc[c], S.scan_tmp2[c]);
-  if (active) {
-    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur < 0 || (cur % S.bpm) != g.ph) S.any = 1;  // inconsistent stream
-  }
-  __syncthreads();
-  if (S.any) {
-    if (t == 0) a.status[k] = FFCV_SAMPLE_CORRUPT;
-  }
-
-  // ------------------------------------------------------------- P5 ----
-  STAMP(5);
-  if (active && g.pos < my_end) {
-    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur >= 0)
-      decode_range<true>(S, words, nwords, g, my_end, nullptr, nullptr, cur, pred, coef);
-  }
-  __syncthreads();
-
-  if (MODE == JM_COEF) {
-    int16_t *o = (int16_t *)a.out + a.out_stride / 2 * k;
-    for (int64_t b = t; b < S.nblocks; b += JT) {
-      int64_t m = b / S.bpm;
-      int ph = (int)(b - m * S.bpm);
-      int my = (int)(m / S.mcux), mx = (int)(m - (int64_t)my * S.mcux);
-      int c = S.blk_comp[ph];
-      int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
-      const uint4 *sp = (const uint4 *)(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64);
-      uint4 *dp = (uint4 *)(o + b * 64);
-      for (int i = 0; i < 8; i++) dp[i] = sp[i];
-    }
-    if (t == 0 && !S.any) a.status[k] = FFCV_SAMPLE_OK;
-    return;
-  }
-
-  // ------------------------------------------------------------- P6 ----
-  STAMP(6);
-  uint8_t *planes = a.planes + a.plane_slot * k;
-  for (int c = 0; c < S.ncomp; c++) {
-    int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
-    int stride = S.bw[c] * 8;
-    for (int i = t; i < wbw * wbh; i += JT) {
-      int by = S.wy0[c] + i / wbw, bx = S.wx0[c] + i % wbw;
-      const int16_t *cp = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
-      int16_t blk[64];
-#pragma unroll
-      for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(blk + p8 * 8) = ((const uint4 *)cp)[p8];
-      idct_ifast_block(blk, S.qmul[c], planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
-    }
-  }
-  __syncthreads();
-
-  // ------------------------------------------------------------- P7 ----
-  STAMP(7);
-  const int rh = S.rh, rw = S.rw, ri = S.ri, rj = S.rj;
-  uint8_t *roi;
-  uint64_t roi_step;
+  const uint8_t *planes = a.planes + a.plane_slot * k;
   if (MODE == JM_FULL) {
-    roi = (uint8_t *)a.out + a.out_stride * k;
-    roi_step = (uint64_t)S.W * 3;
-  } else {
-    roi = a.roi + a.roi_slot * k;
-    roi_step = (uint64_t)rw * 3;
+    uint8_t *o = (uint8_t *)ob;
+    for (int i = t; i < (oy1 - oy0) * out_w; i += K2T) {
+      int y = oy0 + i / out_w, x = i % out_w;
+      int v[3];
+      pixel_rgb(I, planes, y, x, v);
+      uint8_t *d = o + ((uint64_t)y * out_w + x) * 3;
+      d[0] = (uint8_t)v[0];
+      d[1] = (uint8_t)v[1];
+      d[2] = (uint8_t)v[2];
+    }
+    return;
   }
-  for (int i = t; i < rh * rw; i += JT) {
-    int y = i / rw, x = i - y * rw;
-    int Y = y + ri, X = x + rj;
+  if (FP16)
+    for (int i = t; i < 768; i += K2T) s_lut[i] = a.p.lut[i];
+  ResizePlan P = make_plan(I.rw, I.rh, out_w, out_h);
+  int r0, r1;
+  band_rows(P, oy0, oy1, &r0, &r1);
+  const int nrows = r1 - r0 + 1;
+  const int step = I.rw * 3;
+  const bool staged = (uint64_t)nrows * step <= (uint64_t)(K2_LDS - (FP16 ? 1536 : 0));
+  // Bands too wide for LDS stage their rows in the image's coefficient slot
+  // (dead once K1 has run) at their absolute crop-row position; rows shared
+  // with a neighbouring band are written with identical bytes by both.
+  uint8_t *groi = (uint8_t *)(a.coef + a.coef_slot * k);
+  uint8_t *dst = staged ? roi : groi + (uint64_t)r0 * step;
+  for (int i = t; i < nrows * I.rw; i += K2T) {
+    int yy = i / I.rw, x = i - yy * I.rw;
     int v[3];
-    if (S.ncomp == 1) {
-      int g0 = planes[S.poff[0] + (uint64_t)Y * (S.bw[0] * 8) + X];
-      v[0] = v[1] = v[2] = g0;
-    } else {
-      int s3[3];
-      for (int c = 0; c < 3; c++)
-        s3[c] = upsample_at(planes + S.poff[c], S.bw[c] * 8, S.cw[c], S.ch[c], S.hmax / S.hs[c],
-                            S.vmax / S.vs[c], Y, X);
-      if (S.color_rgb) {
-        v[0] = s3[0];
-        v[1] = s3[1];
-        v[2] = s3[2];
-      } else {
-        ycc_rgb(s3[0], s3[1], s3[2], v);
-      }
-    }
-    uint8_t *o = roi + (uint64_t)y * roi_step + (uint64_t)x * 3;
-    o[0] = (uint8_t)v[0];
-    o[1] = (uint8_t)v[1];
-    o[2] = (uint8_t)v[2];
-  }
-  if (MODE == JM_FULL) {
-    if (t == 0 && !S.any) a.status[k] = FFCV_SAMPLE_OK;
-    return;
+    pixel_rgb(I, planes, I.ri + r0 + yy, I.rj + x, v);
+    uint8_t *d = dst + (uint64_t)yy * step + x * 3;
+    d[0] = (uint8_t)v[0];
+    d[1] = (uint8_t)v[1];
+    d[2] = (uint8_t)v[2];
   }
   __syncthreads();
-
-  // ------------------------------------------------------------- P8 ----
-  STAMP(8);
-  __shared__ uint16_t s_lut[FP16 ? 768 : 1];
-  if (FP16) {
-    for (int i = t; i < 768; i += JT) s_lut[i] = a.p.lut[i];
-    __syncthreads();
-  }
-  RoiScratch rs{roi, roi_step};
-  ResizePlan P = make_plan(rw, rh, a.p.out_w, a.p.out_h);
   Epilogue ep;
-  ep.out_h = a.p.out_h;
-  ep.out_w = a.p.out_w;
+  ep.out_h = out_h;
+  ep.out_w = out_w;
   ep.cut_size = a.cut ? a.p.cutout_size : 0;
   ep.cut_y = a.cut ? a.cut[2 * k] : 0;
   ep.cut_x = a.cut ? a.cut[2 * k + 1] : 0;
@@ -1004,32 +1159,34 @@ __global__ void __launch_bounds__(JT) jpeg_kernel(JpegArgs a) {
   ep.fill[0] = a.p.cutout_fill[0];
   ep.fill[1] = a.p.cutout_fill[1];
   ep.fill[2] = a.p.cutout_fill[2];
-  const int npx = a.p.out_h * a.p.out_w;
-  char *ob = (char *)a.out + a.out_stride * k;
-  for (int px = t; px < npx; px += JT) {
-    int dy = px / a.p.out_w, dx = px - dy * a.p.out_w;
+  LdsRoi lr{roi, r0, step};
+  RoiSrc gr{groi, (uint64_t)step};
+  const int npx = (oy1 - oy0) * out_w;
+  for (int i = t; i < npx; i += K2T) {
+    int dy = oy0 + i / out_w, dx = i % out_w;
     int v[3];
     if (ep.in_cut(dy, dx)) {
       v[0] = ep.fill[0];
       v[1] = ep.fill[1];
       v[2] = ep.fill[2];
+    } else if (staged) {
+      resize_pixel(P, lr, dy, ep.src_x(dx), v);
     } else {
-      resize_pixel(P, rs, dy, ep.src_x(dx), v);
+      resize_pixel(P, gr, dy, ep.src_x(dx), v);
     }
+    uint64_t px = (uint64_t)dy * out_w + dx;
     if (FP16) {
-      uint16_t *o = (uint16_t *)ob + (uint64_t)px * 3;
+      uint16_t *o = (uint16_t *)ob + px * 3;
       o[0] = s_lut[v[0] * 3];
       o[1] = s_lut[v[1] * 3 + 1];
       o[2] = s_lut[v[2] * 3 + 2];
     } else {
-      uint8_t *o = (uint8_t *)ob + (uint64_t)px * 3;
+      uint8_t *o = (uint8_t *)ob + px * 3;
       o[0] = (uint8_t)v[0];
       o[1] = (uint8_t)v[1];
       o[2] = (uint8_t)v[2];
     }
   }
-  STAMP(9);
-  if (t == 0 && !S.any) a.status[k] = FFCV_SAMPLE_OK;
 }
 
 // ---------------------------------------------------------------- ctx -----
@@ -1044,11 +1201,21 @@ struct ffcv_jpeg_ctx {
   uint64_t coef_slot;
   uint8_t *planes;
   uint64_t plane_slot;
-  uint8_t *roi;
-  uint64_t roi_slot;
+  int16_t *dcd;
+  uint64_t dcd_slot;
+  ImgInfo *info;
 };
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+static void free_ctx(ffcv_jpeg_ctx *c) {
+  (void)hipFree(c->dstuff);
+  (void)hipFree(c->coef);
+  (void)hipFree(c->planes);
+  (void)hipFree(c->dcd);
+  (void)hipFree(c->info);
+  delete c;
+}
 
 extern "C" {
 
@@ -1064,24 +1231,20 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
   c->max_h = max_height;
   c->max_w = max_width;
   c->max_bytes = max_bytes;
-  // blocks of all components, MCU padded (hmax, vmax <= 4)
   uint64_t bw = (max_width + 7) / 8 + 4, bh = (max_height + 7) / 8 + 4;
-  uint64_t nblk = 3 * bw * bh;
+  uint64_t nblk = 3 * bw * bh;  // all components, MCU padded (hmax, vmax <= 4)
   c->dstuff_slot = align_up(max_bytes + 64, 256);
-  c->coef_slot = align_up(nblk * 64, 128);         // int16 elements
-  c->plane_slot = align_up(nblk * 64, 256);        // bytes
-  c->roi_slot = align_up((uint64_t)max_height * max_width * 3, 256);
+  c->coef_slot = align_up(nblk * 64, 128);   // int16 elements
+  c->plane_slot = align_up(nblk * 64, 256);  // bytes
+  c->dcd_slot = align_up(nblk, 128);         // int16 elements
   hipError_t e;
   if ((e = hipMalloc(&c->dstuff, c->dstuff_slot * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->coef, c->coef_slot * 2 * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->planes, c->plane_slot * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->roi, c->roi_slot * max_batch)) != hipSuccess) {
+      (e = hipMalloc(&c->dcd, c->dcd_slot * 2 * max_batch)) != hipSuccess ||
+      (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess) {
     int rc = ffcv::check_hip(e, "ffcv_jpeg_create: hipMalloc");
-    (void)hipFree(c->dstuff);
-    (void)hipFree(c->coef);
-    (void)hipFree(c->planes);
-    (void)hipFree(c->roi);
-    delete c;
+    free_ctx(c);
     return rc;
   }
   *out = c;
@@ -1097,12 +1260,7 @@ int ffcv_jpeg_set_debug(ffcv_jpeg_ctx *c, uint64_t *dbg) {
 }
 
 int ffcv_jpeg_destroy(ffcv_jpeg_ctx *c) {
-  if (!c) return FFCV_OK;
-  (void)hipFree(c->dstuff);
-  (void)hipFree(c->coef);
-  (void)hipFree(c->planes);
-  (void)hipFree(c->roi);
-  delete c;
+  if (c) free_ctx(c);
   return FFCV_OK;
 }
 
@@ -1117,8 +1275,9 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.coef_slot = c->coef_slot;
   a.planes = c->planes;
   a.plane_slot = c->plane_slot;
-  a.roi = c->roi;
-  a.roi_slot = c->roi_slot;
+  a.dcd = c->dcd;
+  a.dcd_slot = c->dcd_slot;
+  a.info = c->info;
   a.max_h = c->max_h;
   a.max_w = c->max_w;
   a.dbg = c->dbg;
@@ -1157,11 +1316,15 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   const bool fp16 = p->lut != nullptr;
   uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
   a.out_stride = p->out_stride ? p->out_stride : dense;
+  hipStream_t s = ffcv::as_stream(stream);
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3(batch), dim3(JT), 0, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
+  dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (fp16)
-    hipLaunchKernelGGL((jpeg_kernel<JM_RRC, true>), dim3(batch), dim3(JT), 0, ffcv::as_stream(stream), a);
+    hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, true>), g2, dim3(K2T), K2_LDS, s, a);
   else
-    hipLaunchKernelGGL((jpeg_kernel<JM_RRC, false>), dim3(batch), dim3(JT), 0, ffcv::as_stream(stream), a);
-  FFCV_LAUNCH_CHECK("jpeg_kernel<RRC>");
+    hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, false>), g2, dim3(K2T), K2_LDS, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<RRC>");
   return FFCV_OK;
 }
 
@@ -1177,8 +1340,12 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   JpegArgs a = make_args(c, base, samples, status);
   a.out = out;
   a.out_stride = out_stride;
-  hipLaunchKernelGGL((jpeg_kernel<JM_FULL, false>), dim3(batch), dim3(JT), 0, ffcv::as_stream(stream), a);
-  FFCV_LAUNCH_CHECK("jpeg_kernel<FULL>");
+  hipStream_t s = ffcv::as_stream(stream);
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3(batch), dim3(JT), 0, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
+  dim3 g2((c->max_h + BAND - 1) / BAND, batch);
+  hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_FULL, false>), g2, dim3(K2T), 0, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<FULL>");
   return FFCV_OK;
 }
 
@@ -1192,8 +1359,8 @@ int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *
   a.out = coefs;
   a.out_stride = max_blocks * 64 * 2;
   a.max_blocks = max_blocks;
-  hipLaunchKernelGGL((jpeg_kernel<JM_COEF, false>), dim3(batch), dim3(JT), 0, ffcv::as_stream(stream), a);
-  FFCV_LAUNCH_CHECK("jpeg_kernel<COEF>");
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3(batch), dim3(JT), 0, ffcv::as_stream(stream), a);
+  FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<COEF>");
   return FFCV_OK;
 }
 

@@ -134,6 +134,8 @@ def main():
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)
+    ap.add_argument('--inflight', type=int, default=2,
+                    help='batches in flight on separate HIP streams (Loader batches_ahead analogue)')
     args = ap.parse_args()
 
     import torch
@@ -193,14 +195,24 @@ def main():
     order = np.resize(perm, need).astype(np.int64)
     d_order = torch.from_numpy(order).to(dev)
 
-    # ---- per-step buffers
-    d_smp = torch.empty(batch * 32, dtype=torch.uint8, device=dev)
-    d_crops = torch.empty((batch, 4), dtype=torch.int32, device=dev)
-    d_cut = torch.empty((batch, 2), dtype=torch.int32, device=dev) if cut else None
-    d_status = torch.empty(batch, dtype=torch.int32, device=dev)
-    d_rstat = torch.empty(batch, dtype=torch.int32, device=dev)
+    # ---- per-slot buffers: --inflight batches overlap on their own HIP
+    # streams (the Loader's batches_ahead slots do the same), each slot with
+    # its own decoder scratch; a slot's next batch is ordered behind its last.
+    K = max(1, args.inflight)
     out_dtype = torch.float16 if norm else torch.uint8
-    outs = [torch.empty((batch, out, out, 3), dtype=out_dtype, device=dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(K)]
+    slots = []
+    for _ in range(K):
+        slots.append({
+            'smp': torch.empty(batch * 32, dtype=torch.uint8, device=dev),
+            'crops': torch.empty((batch, 4), dtype=torch.int32, device=dev),
+            'cut': torch.empty((batch, 2), dtype=torch.int32, device=dev) if cut else None,
+            'status': torch.empty(batch, dtype=torch.int32, device=dev),
+            'rstat': torch.empty(batch, dtype=torch.int32, device=dev),
+            'out': torch.empty((batch, out, out, 3), dtype=out_dtype, device=dev),
+            'dec': (L.JpegDecoder(batch, int(hs.max()), int(ws.max()), int(sizes.max()))
+                    if mode == 'jpg' else None),
+        })
     d_lut = None
     rp = L.RRCParams()
     rp.out_h = rp.out_w = out
@@ -219,31 +231,31 @@ def main():
     dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
     dp.loader_seed = 0
     dp.epoch = 0
-    dec = None
-    if mode == 'jpg':
-        dec = L.JpegDecoder(batch, int(hs.max()), int(ws.max()), int(sizes.max()))
-    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize()
 
     def step(i, ev=None):
+        sl = slots[i % K]
+        stream = streams[i % K]
         ids = d_order[i * batch:(i + 1) * batch]
-        L.gather_samples(d_table, ids, d_smp, stream)
-        L.draw_batch(ids, d_smp, dp, d_crops, d_cut, None, d_rstat, stream)
-        o = outs[i & 1]
+        L.gather_samples(d_table, ids, sl['smp'], stream)
+        L.draw_batch(ids, sl['smp'], dp, sl['crops'], sl['cut'], None, sl['rstat'], stream)
         if ev is not None:
             ev[0].record(stream)
-        if dec is not None:
-            dec.rrc(d_data, d_smp, batch, d_crops, d_cut, None, rp, o, d_status, stream)
+        if sl['dec'] is not None:
+            sl['dec'].rrc(d_data, sl['smp'], batch, sl['crops'], sl['cut'], None, rp, sl['out'], sl['status'],
+                          stream)
         else:
-            L.rrc_raw_batch(d_data, d_smp, batch, d_crops, d_cut, None, rp, o, stream)
+            L.rrc_raw_batch(d_data, sl['smp'], batch, sl['crops'], sl['cut'], None, rp, sl['out'], stream)
         if ev is not None:
             ev[1].record(stream)
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    if dec is not None:
-        st = d_status.cpu().numpy()
-        assert (st == 0).all(), f'decode status {np.unique(st)}'
+    if mode == 'jpg':
+        for sl in slots:
+            st = sl['status'].cpu().numpy()
+            assert (st == 0).all(), f'decode status {np.unique(st)}'
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
     if dist:
@@ -269,7 +281,7 @@ def main():
         roof_note = 'S_jpeg + 224*224*3*2 (fp16 out) per image (SURVEY 8d C3)'
     else:
         # crop ROI read (E[h*w]/(H*W) measured per batch below) + output write
-        crops_np = d_crops.cpu().numpy()
+        crops_np = slots[0]['crops'].cpu().numpy()
         unit_bytes = float((crops_np[:, 2].astype(np.float64) * crops_np[:, 3] * 3).mean()) + out * out * 3
         roof_note = '3*h*w crop ROI read + 448*448*3 write per image (SURVEY 8d C5)'
     achieved = unit_bytes * batch / (kern_ms * 1e-3) / 1e9
@@ -287,7 +299,7 @@ def main():
         'dtype': 'u8',
         'data': f'synthetic ({U} unique encodings replicated to {N} HBM-resident samples)',
         'config': {'workload': WORKLOAD[args.config], 'global_batch': batch * world,
-                   'per_gpu_batch': batch, 'dataset_size': N, 'mean_sample_bytes': round(mean_bytes, 1),
+                   'per_gpu_batch': batch, 'inflight_batches': K, 'dataset_size': N, 'mean_sample_bytes': round(mean_bytes, 1),
                    'parallelism': f'dp{world} (traversal-order sharding, no collectives)'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': None,

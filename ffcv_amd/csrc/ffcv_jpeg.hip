@@ -8,14 +8,23 @@
 //
 // Two launches per batch:
 //
-// K1 jpeg_entropy_kernel -- one 256-lane workgroup per image:
-//   P0  the first 4 KB of the file are staged in LDS; one lane walks the
-//       markers there (SOF/DHT/DQT/DRI/SOS), validates geometry and tables
-//   P1  Huffman lookup tables (10-bit fast LUT + canonical slow path) and
-//       the ifast dequantisation multipliers (jddctmgr.c), in LDS
-//   P2  de-stuffing (0xFF00 -> 0xFF) of the entropy-coded segment in one
-//       read pass + workgroup scan + one write pass, into an LDS-resident
-//       word stream (images above 24 KB of entropy data use HBM scratch)
+// K1 jpeg_entropy_kernel -- ONE WAVE (64 lanes) per image, ~26 KB of LDS, so
+// six images decode concurrently per CU.  (A self-synchronising Huffman
+// decode costs about the same latency at 64 or 256 lanes per image -- the
+// latency is the resynchronisation distance -- but a third of the lane-steps
+// at 64, so the wave-per-image shape triples throughput.)
+//   P0  the first 2 KB of the file are staged in LDS; one lane walks the
+//       markers (SOF/DHT/DQT/DRI/SOS), validates geometry and tables, and
+//       hands out Huffman table slots and LUT space
+//   P1  Huffman decode tables (jdhuff.c jpeg_make_d_derived_tbl, with its
+//       checks): per slot an 11-bit (AC) or 9-bit (DC) first-level LUT whose
+//       entry gives code length, extra-bit count and coefficient advance, a
+//       5-bit second level for longer codes, canonical limits for the rest;
+//       ifast dequantisation multipliers (jddctmgr.c)
+//   P2  de-stuffing (0xFF00 -> 0xFF) of the entropy-coded segment in stream
+//       order, one coalesced dword per lane per step with a wave scan of the
+//       kept-byte counts, into an L2-resident scratch stream (zero-padded:
+//       libjpeg fills zeros after a marker)
 //   P3  self-synchronising parallel Huffman decode.  The stream is cut into
 //       one bit range per lane; a lane decodes its range from a guessed state
 //       (bit position, coefficient index z, block-in-MCU), records where its
@@ -23,15 +32,14 @@
 //       further round gives lane t the exit state of lane t-1; a lane whose
 //       guess changed re-decodes only until it reaches a block start it
 //       recorded before (same bit position and MCU phase: from there its old
-//       trajectory is exact), so a round costs the resynchronisation
-//       distance, not a full range.  Lane 0 is exact, so round r fixes lanes
-//       0..r at worst; rounds end when no guess changes.
-//   P4  workgroup scan of blocks-started -> each lane's first block index
+//       trajectory is exact).  Lane 0 is exact, so round r fixes lanes 0..r
+//       at worst; rounds end when no guess changes.
+//   P4  wave scan of blocks-started -> each lane's first block index
 //   P5  second decode: DC differences of every block, quantised AC
-//       coefficients (natural order) of the blocks the crop window needs
-//   P6  per-component DC prediction as a workgroup prefix scan
-//   P7  dequantise + ifast IDCT (jidctfst.c) of the window's blocks ->
-//       component planes in HBM scratch; per-image geometry record for K2
+//       coefficients (zigzag order) of the blocks the crop window needs
+//   P6  per-component DC prediction as a wave prefix scan
+//   P7  de-zigzag + dequantise + ifast IDCT (jidctfst.c) of the window's
+//       blocks -> component planes in HBM scratch; geometry record for K2
 //
 // K2 jpeg_color_resize_kernel -- one workgroup per band of 16 output rows:
 //   stages the band's source rows of the crop as RGB in LDS (jdsample.c
@@ -45,12 +53,17 @@
 #include "api_internal.h"
 #include "device_common.h"
 
-#define JT 256
-#define FAST_BITS 10
+#define JT 64           // lanes per image (one wave)
+#define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
+#define LUT_POOL 6144   // first-level LUT entries shared by the slots
+#define FB_AC 11        // first-level bits, AC tables
+#define FB_DC 9         // first-level bits, DC tables
+#define SUBB 5          // second-level bits
+#define NSUB 8          // second-level tables per slot
+#define NSLOT 6         // Huffman tables a scan can reference (3 DC + 3 AC)
 #define NTAB 8
-#define HDR_BYTES 4096
-#define LDS_STREAM_BYTES 24576
-#define NEV 16
+#define NEV 10
+#define STREAM_PAD 32   // zero bytes after the de-stuffed stream
 #define BAND 16
 #define K2T 256
 #define K2_LDS 49152
@@ -65,7 +78,11 @@ struct ImgInfo {
   int32_t cw[3], ch[3], stride[3];
   int32_t ri, rj, rh, rw;
   uint64_t poff[3];
-  int32_t pad[2];
+  // for the IDCT kernel: the window (in blocks) and block layout per
+  // component, and the ifast multipliers
+  int32_t wx0[3], wy0[3], wbw[3], wbh[3], bw[3];
+  uint64_t coff[3];
+  int16_t qmul[3][64];
 };
 
 struct JShared {
@@ -76,7 +93,13 @@ struct JShared {
   int mcux, mcuy, bpm, nblocks;
   int cw[3], ch[3], bw[3], bh[3];
   int blk_comp[10], blk_dx[10], blk_dy[10];
-  int ph_dc[10], ph_ac[10];  // table index per block-in-MCU
+  // Huffman table slots referenced by the scan (AC first); per block-in-MCU
+  // slot numbers packed 3 bits per phase; per slot LUT base and bits
+  int nslots;
+  int slot_tab[NSLOT];  // class * 4 + id
+  uint32_t sinfo[NSLOT];  // base | bits << 16 | slot << 20
+  uint32_t dinf[10], ainf[10];  // sinfo of each block-in-MCU's DC / AC table
+  uint32_t dcpack, acpack, acmask;
   uint32_t scan_off;
   uint32_t dqt_off[4];
   int dqt_prec[4], dqt_ok[4];
@@ -88,35 +111,42 @@ struct JShared {
   int wx0[3], wx1[3], wy0[3], wy1[3];
   uint64_t coff[3];
   uint64_t poff[3];
-  uint32_t first_marker;
   uint32_t dlen;
   int any;
-  // tables
-  uint16_t lut[NTAB][1 << FAST_BITS];
-  int32_t maxcode[NTAB][18];
-  int32_t valoff[NTAB][17];
-  uint8_t vals[NTAB][256];
+  // per block-in-MCU descriptor for the write pass: block index of MCU (0,0)
+  // in its component's plane, blocks per MCU row step, hs, and the window
+  // as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
+  int4 pdesc[10][2];
+  // decode tables
+  uint32_t lim[NSLOT][17];  // left-justified end of length-l codes
+  int32_t valoff[NSLOT][17];
+  uint8_t vals[NSLOT][256];
   int16_t qmul[3][64];
-  uint8_t nat[80];
-  // lanes
-  uint32_t e_pos[JT];
-  uint16_t e_zph[JT];
-  uint32_t scan_tmp[JT];
+  int nsub[NSLOT];
+  uint16_t sub_prefix[NSLOT][NSUB];
+  // decode entry: (len-1) | size << 4 | zinc << 8; 0x8000 | n = second-level
+  // table n; 0 = canonical slow path
+  uint16_t lut2[NSLOT][NSUB][1 << SUBB];
   int32_t scan3[3][JT];
-  uint32_t ev[NEV][JT];  // block-start events: pos << 4 | phase
-  uint8_t nev[JT];
-  // header bytes, then the de-stuffed stream (same storage)
+  uint32_t ev[2][NEV + 1][JT];  // block-start events (pos << 4 | phase), double-buffered
+  // header bytes, then the first-level LUT pool (same storage)
   union {
     uint8_t hdr[HDR_BYTES];
-    uint32_t stream[LDS_STREAM_BYTES / 4];
+    uint16_t lut[LUT_POOL];
   } u;
 };
 
-__constant__ uint8_t c_natural[80] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
-    40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
-    29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
-    47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+// zigzag index of each natural (row-major) coefficient position; the entropy
+// pass stores coefficients in zigzag order
+constexpr uint8_t kZigzagOfNatural[64] = {
+    0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42, 3,  8,  12, 17, 25, 30,
+    41, 43, 9,  11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38,
+    46, 51, 55, 60, 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+__constant__ uint8_t c_natural[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
 __constant__ int32_t c_aanscales[64] = {
     16384, 22725, 21407, 19266, 16384, 12873, 8867,  4520,  22725, 31521, 29692, 26722, 22725,
@@ -126,45 +156,35 @@ __constant__ int32_t c_aanscales[64] = {
     8867,  6967,  4799,  2446,  4520,  6270,  5906,  5315,  4520,  3552,  2446,  1247};
 
 // ------------------------------------------------------------ bit reader --
-// The de-stuffed stream is big-endian bytes stored as 32-bit words, either in
-// LDS or (large images) in HBM scratch; reads past the end return zeros.
-struct LdsWords {
-  const uint32_t *w;
-  uint32_t nw;
-  FFCV_DEV uint32_t ld(uint32_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
-};
-struct GlobalWords {
-  const uint32_t *w;
-  uint32_t nw;
-  FFCV_DEV uint32_t ld(uint32_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
-};
-
-template <class Src>
+// The de-stuffed stream: big-endian bytes read as 32-bit words from the
+// image's scratch slot (L2-resident: written in P2, re-read every round),
+// zero-padded by STREAM_PAD bytes so no read needs a bounds check.  The
+// reader holds 33..64 valid bits plus the next word, loaded right after a
+// refill and consumed at the following one (~5 symbols later), so a symbol
+// (code <= 16 bits + <= 15 extra bits) never waits on memory.
 struct BitReader {
-  Src src;
+  const uint32_t *w;
   uint64_t acc;
   int nb;
   uint32_t wi;
-  uint32_t pos;
-  FFCV_DEV void init(const Src &s, uint32_t p) {
-    src = s;
+  uint32_t nxt;  // raw (little-endian) next word: swapped only when used, so
+                 // its load is waited for at the next refill, not here
+  FFCV_DEV void init(const uint32_t *words, uint32_t p) {
+    w = words;
     wi = p >> 5;
-    acc = ((uint64_t)src.ld(wi) << 32) | (uint64_t)src.ld(wi + 1);
-    acc <<= (p & 31);
+    uint32_t w0 = __builtin_bswap32(w[wi]), w1 = __builtin_bswap32(w[wi + 1]);
+    nxt = w[wi + 2];
+    acc = (((uint64_t)w0 << 32) | (uint64_t)w1) << (p & 31);
     nb = 64 - (int)(p & 31);
     wi += 2;
-    pos = p;
   }
-  FFCV_DEV uint32_t peek16() const { return (uint32_t)(acc >> 48); }
-  FFCV_DEV uint32_t peek(int n) const { return n ? (uint32_t)(acc >> (64 - n)) : 0u; }
   FFCV_DEV void consume(int n) {
     acc <<= n;
     nb -= n;
-    pos += n;
     if (nb <= 32) {
-      acc |= (uint64_t)src.ld(wi) << (32 - nb);
-      wi++;
+      acc |= (uint64_t)__builtin_bswap32(nxt) << (32 - nb);
       nb += 32;
+      nxt = w[++wi];
     }
   }
 };
@@ -177,181 +197,208 @@ struct DecState {
   int ph;  // block index inside the MCU
 };
 
-// One Huffman symbol of table ti (LUT length 0 -> canonical slow path,
-// jdhuff.c jpeg_huff_decode).
-template <class Src>
-FFCV_DEV int huff_sym(const JShared &S, int ti, BitReader<Src> &br) {
-  uint32_t look = br.peek16();
-  uint32_t e = S.lut[ti][look >> (16 - FAST_BITS)];
-  int len = (int)(e >> 8);
-  int sym = (int)(e & 0xff);
-  if (len == 0) {
-    len = 16;
-    sym = 0;
-    for (int l = FAST_BITS + 1; l <= 16; l++) {
-      int code = (int)(look >> (16 - l));
-      if (code <= S.maxcode[ti][l]) {
-        sym = S.vals[ti][(S.valoff[ti][l] + code) & 0xff];
-        len = l;
-        break;
-      }
-    }
+// Symbol -> decode entry.  DC: size = symbol, z 0 -> 1.  AC: size = low
+// nibble; z advances by run+1, by 16 for ZRL, past the block for EOB.
+FFCV_DEV uint32_t make_entry(bool ac, int len, int sym) {
+  int size, zinc;
+  if (!ac) {
+    size = sym;
+    zinc = 1;
+  } else {
+    size = sym & 15;
+    int r = sym >> 4;
+    zinc = size ? r + 1 : (r == 15 ? 16 : 127);
   }
-  br.consume(len);
-  return sym;
+  return (uint32_t)(len - 1) | ((uint32_t)size << 4) | ((uint32_t)zinc << 8);
 }
 
-// SYNC decode of a lane's range [st.pos, end_bit): counts blocks started and
-// records their start events.  With old_nev >= 0 (a later round) it stops at
-// the first block start matching an event of the lane's previous trajectory
-// and splices: count and exit state come from the old run.
-template <class Src>
-FFCV_DEV DecState sync_range(JShared &S, const Src &src, DecState st, uint32_t end_bit, int lane,
-                             uint32_t *count, DecState old_exit, uint32_t old_count, int old_nev) {
-  BitReader<Src> br;
-  br.init(src, st.pos);
+// Canonical decode of a 16-bit lookahead (jdhuff.c jpeg_huff_decode): the
+// code length is the first l with look < lim[l]; past lim[16] the code is
+// invalid and, like libjpeg, yields symbol 0 after 16 bits.
+FFCV_DEV uint32_t slow_entry(const JShared &S, int slot, uint32_t look) {
+  int len = 1;
+#pragma unroll
+  for (int l = 1; l < 16; l++) len += look >= S.lim[slot][l];
+  int sym = 0;
+  if (look < S.lim[slot][16]) sym = S.vals[slot][(S.valoff[slot][len] + (int)(look >> (16 - len))) & 0xff];
+  else len = 16;
+  return make_entry((S.acmask >> slot) & 1, len, sym);
+}
+
+// inf = sinfo of the table: LUT base | bits << 16 | slot << 20 (bits 0: none)
+FFCV_DEV uint32_t decode_entry(const JShared &S, uint32_t inf, uint64_t acc) {
+  const uint32_t look = (uint32_t)(acc >> 48);
+  const int bits = (int)((inf >> 16) & 15), slot = (int)(inf >> 20);
+  uint32_t e = S.u.lut[(inf & 0xffff) + (look >> (16 - bits))];
+  e = bits ? e : 0u;
+  if (e & 0x8000u) e = S.lut2[slot][e & (NSUB - 1)][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
+  if (e == 0) e = slow_entry(S, slot, look);
+  return e;
+}
+
+FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 7); }
+
+// SYNC decode of a lane's range [st.pos, end_bit): counts the blocks started
+// in it and records their start events (the first NEV; row NEV is a dummy
+// the overflow writes go to).  With use_old (a later round) it stops at a
+// block start that matches an event of the lane's previous trajectory and
+// splices onto it: from an identical state the old trajectory is exact, so
+// its remaining count and exit state are reused.  The old-event cursor
+// advances one event per symbol (old events behind the decode position can
+// never match); lagging only delays a splice, never makes a wrong one.
+// Events are double-buffered: buffer cb holds the previous trajectory's,
+// cb ^ 1 receives the new one.
+FFCV_DEV DecState sync_range(JShared &S, const uint32_t *words, DecState st,
+                             uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, DecState old_exit,
+                             bool use_old, uint32_t &iters) {
+  BitReader br;
+  br.init(words, st.pos);
+  uint32_t pos = st.pos;
   int z = st.z, ph = st.ph;
-  int dco = S.ph_dc[ph], aco = S.ph_ac[ph];
-  uint32_t started = 0;
-  uint32_t evs[NEV];
-  int n_new = 0;
+  const int bpm = S.bpm;
+  // table infos of this phase and (prefetched) of the next
+  uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
+  int nph = ph + 1 == bpm ? 0 : ph + 1;
+  uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
+  const int ob = cb, nbuf = cb ^ 1;
+  const int onev = use_old ? nev : 0;
   int j = 0;
-  while (br.pos < end_bit) {
-    if (z == 0) {
-      if (old_nev > 0) {
-        uint32_t key = (br.pos << 4) | (uint32_t)ph;
-        while (j < old_nev && S.ev[j][lane] < key) j++;
-        if (j < old_nev && S.ev[j][lane] == key) {
-          // spliced onto the previous trajectory at its j-th block start
-          int keep = min(old_nev - j, NEV - n_new);
-          if (n_new < j) {
-            for (int q = 0; q < keep; q++) S.ev[n_new + q][lane] = S.ev[j + q][lane];
-          } else if (n_new > j) {
-            for (int q = keep - 1; q >= 0; q--) S.ev[n_new + q][lane] = S.ev[j + q][lane];
-          }
-          for (int q = 0; q < n_new; q++) S.ev[q][lane] = evs[q];
-          S.nev[lane] = (uint8_t)(n_new + keep);
-          *count = started + (old_count - (uint32_t)j);
-          return old_exit;
-        }
+  uint32_t ocur = onev > 0 ? S.ev[ob][0][lane] : 0xFFFFFFFFu;
+  int n = 0;
+  bool spliced = false;
+  while (pos < end_bit) {
+    iters++;
+    const bool isblk = z == 0;
+    const uint32_t key = (pos << 4) | (uint32_t)ph;
+    const uint32_t onext = S.ev[ob][min(j + 1, NEV)][lane];
+    if (isblk) {
+      if (ocur == key) {
+        spliced = true;
+        break;
       }
-      if (n_new < NEV) evs[n_new++] = (br.pos << 4) | (uint32_t)ph;
-      started++;
+      S.ev[nbuf][min(n, NEV)][lane] = key;
+      n++;
     }
-    int ti = z == 0 ? dco : aco;
-    int sym = huff_sym(S, ti, br);
-    int s = z == 0 ? sym : (sym & 15);
-    int r = z == 0 ? 0 : (sym >> 4);
-    br.consume(s);
-    int zac = s ? z + r + 1 : (r == 15 ? z + 16 : 64);
-    z = z == 0 ? 1 : zac;
+    const bool adv = ocur < key;
+    j += adv ? 1 : 0;
+    ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
+    const uint32_t e = decode_entry(S, isblk ? dinf : ainf, br.acc);
+    const int nbits = (int)(e & 15) + 1 + ((int)(e >> 4) & 15);
+    br.consume(nbits);
+    pos += nbits;
+    z += (int)(e >> 8);
     if (z >= 64) {
       z = 0;
-      ph = ph + 1 == S.bpm ? 0 : ph + 1;
-      dco = S.ph_dc[ph];
-      aco = S.ph_ac[ph];
+      ph = nph;
+      dinf = ndinf;
+      ainf = nainf;
+      nph = ph + 1 == bpm ? 0 : ph + 1;
+      ndinf = S.dinf[nph];
+      nainf = S.ainf[nph];
     }
   }
-  for (int q = 0; q < n_new; q++) S.ev[q][lane] = evs[q];
-  S.nev[lane] = (uint8_t)n_new;
-  *count = started;
+  if (spliced) {  // at the previous trajectory's j-th block start
+    int m = n;
+    if (n < NEV) {
+      int keep = min(onev - j, NEV - n);
+      for (int q = 0; q < keep; q++) S.ev[nbuf][n + q][lane] = S.ev[ob][j + q][lane];
+      m = n + keep;
+    }
+    nev = min(m, NEV);
+    cnt = (uint32_t)n + (cnt - (uint32_t)j);
+    cb = nbuf;
+    return old_exit;
+  }
+  nev = min(n, NEV);
+  cnt = (uint32_t)n;
+  cb = nbuf;
   DecState out;
-  out.pos = br.pos;
+  out.pos = pos;
   out.z = z;
   out.ph = ph;
   return out;
 }
 
-// WRITE decode: DC differences of every block and AC coefficients of the
-// blocks inside the window.  blk = index of the block in progress (z > 0) or
-// of the next block to start (z == 0).
-template <class Src>
-FFCV_DEV void write_range(JShared &S, const Src &src, DecState st, uint32_t end_bit, int64_t blk,
-                          int16_t *coef, int16_t *dcd) {
-  BitReader<Src> br;
-  br.init(src, st.pos);
+// WRITE decode: DC differences of every block and the AC coefficients (in
+// zigzag order; the IDCT de-zigzags in registers) of the blocks inside the
+// window.  blk = index of the block in progress (z > 0) or of the next block
+// to start (z == 0).  The next phase's descriptor is prefetched one block
+// ahead, so a block start costs no LDS round trip; each symbol makes at most
+// one (predicated) 2-byte store.
+FFCV_DEV void write_range(JShared &S, const uint32_t *words, DecState st, uint32_t end_bit,
+                          int64_t blk, int16_t *coef, int16_t *dcd, uint32_t &iters) {
+  BitReader br;
+  br.init(words, st.pos);
+  uint32_t pos = st.pos;
   int z = st.z, ph = st.ph;
-  int dco = S.ph_dc[ph], aco = S.ph_ac[ph];
-  const int nblocks = S.nblocks;
-  int m = (int)(blk / S.bpm);
-  int my = m / S.mcux, mx = m - my * S.mcux;
+  const int bpm = S.bpm, mcux = S.mcux;
+  const int64_t nblocks = S.nblocks;
+  uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
+  int nph0 = ph + 1 == bpm ? 0 : ph + 1;
+  uint32_t ndinf = S.dinf[nph0], nainf = S.ainf[nph0];
+  int m = (int)(blk / bpm);
+  int my = m / mcux, mx = m - my * mcux;
   int16_t *bptr = coef;
   bool inwin = false;
+  int4 pd0 = S.pdesc[ph][0], pd1 = S.pdesc[ph][1];
   auto locate = [&]() {
-    int c = S.blk_comp[ph];
-    int bx = mx * S.hs[c] + S.blk_dx[ph];
-    int by = my * S.vs[c] + S.blk_dy[ph];
-    inwin = blk < nblocks && bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c];
-    bptr = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
+    // pd0 = {base block, blocks per MCU row, hs, mx_lo}, pd1 = {mx_hi, my_lo, my_hi, -}
+    inwin = blk < nblocks && mx >= pd0.w && mx <= pd1.x && my >= pd1.y && my <= pd1.z;
+    bptr = coef + ((uint64_t)(uint32_t)pd0.x + (uint64_t)my * (uint32_t)pd0.y + (uint64_t)mx * pd0.z) * 64;
+    const int nph = ph + 1 == bpm ? 0 : ph + 1;
+    pd0 = S.pdesc[nph][0];
+    pd1 = S.pdesc[nph][1];
   };
   if (z > 0) locate();
-  while (br.pos < end_bit) {
-    if (z == 0) {
+  while (pos < end_bit) {
+    iters++;
+    const bool isblk = z == 0;
+    if (isblk) {
       if (blk >= nblocks) break;
       locate();
     }
-    int ti = z == 0 ? dco : aco;
-    int sym = huff_sym(S, ti, br);
-    int s = z == 0 ? sym : (sym & 15);
-    int r = z == 0 ? 0 : (sym >> 4);
-    int v = s ? huff_extend((int)br.peek(s), s) : 0;
-    br.consume(s);
-    if (z == 0) {
-      dcd[blk] = (int16_t)v;
-    } else if (s && inwin) {
-      bptr[S.nat[z + r]] = (int16_t)v;
-    }
-    int zac = s ? z + r + 1 : (r == 15 ? z + 16 : 64);
-    z = z == 0 ? 1 : zac;
+    const uint32_t e = decode_entry(S, isblk ? dinf : ainf, br.acc);
+    const int len = (int)(e & 15) + 1, size = (int)(e >> 4) & 15, zinc = (int)(e >> 8);
+    const int raw = (int)((br.acc << len) >> 1 >> (63 - size));
+    const int v = size ? huff_extend(raw, size) : 0;
+    br.consume(len + size);
+    pos += len + size;
+    int16_t *dst = isblk ? dcd + blk : bptr + min(z + zinc - 1, 63);
+    if (isblk || (size && inwin)) *dst = (int16_t)v;
+    z += zinc;
     if (z >= 64) {
       z = 0;
       blk++;
       ph++;
-      if (ph == S.bpm) {
+      if (ph == bpm) {
         ph = 0;
-        if (++mx == S.mcux) {
+        if (++mx == mcux) {
           mx = 0;
           my++;
         }
       }
-      dco = S.ph_dc[ph];
-      aco = S.ph_ac[ph];
+      dinf = ndinf;
+      ainf = nainf;
+      const int np = ph + 1 == bpm ? 0 : ph + 1;
+      ndinf = S.dinf[np];
+      nainf = S.ainf[np];
     }
   }
 }
 
-FFCV_DEV uint32_t wg_exscan_u32(uint32_t v, uint32_t *tmp) {
-  const int t = threadIdx.x;
-  tmp[t] = v;
-  __syncthreads();
+// Exclusive prefix sum over the wave.
+FFCV_DEV uint32_t wave_exscan(uint32_t v) {
+  const int lane = threadIdx.x;
+  uint32_t x = v;
+#pragma unroll
   for (int off = 1; off < JT; off <<= 1) {
-    uint32_t x = t >= off ? tmp[t - off] : 0u;
-    __syncthreads();
-    tmp[t] += x;
-    __syncthreads();
+    uint32_t y = __shfl_up(x, off);
+    x += lane >= off ? y : 0u;
   }
-  uint32_t incl = tmp[t];
-  __syncthreads();
-  return incl - v;
+  return x - v;
 }
+FFCV_DEV int32_t wave_exscan_i(int32_t v) { return (int32_t)wave_exscan((uint32_t)v); }
 
-FFCV_DEV void wg_exscan3(int32_t v[3], int32_t (*tmp)[JT]) {
-  const int t = threadIdx.x;
-  for (int c = 0; c < 3; c++) tmp[c][t] = v[c];
-  __syncthreads();
-  for (int off = 1; off < JT; off <<= 1) {
-    int32_t x0 = t >= off ? tmp[0][t - off] : 0;
-    int32_t x1 = t >= off ? tmp[1][t - off] : 0;
-    int32_t x2 = t >= off ? tmp[2][t - off] : 0;
-    __syncthreads();
-    tmp[0][t] += x0;
-    tmp[1][t] += x1;
-    tmp[2][t] += x2;
-    __syncthreads();
-  }
-  for (int c = 0; c < 3; c++) v[c] = tmp[c][t] - v[c];
-  __syncthreads();
-}
 
 // libjpeg post-IDCT range limit: table[x & 1023] (jdmaster.c)
 FFCV_DEV uint8_t idct_rl(int x) {
@@ -452,6 +499,7 @@ struct JpegArgs {
   uint64_t plane_slot;
   int16_t *dcd;
   uint64_t dcd_slot;
+  uint8_t *rgb;
   ImgInfo *info;
   uint32_t max_h, max_w;
   uint64_t max_blocks;
@@ -468,7 +516,14 @@ struct JpegArgs {
 // P0 (one lane): marker walk over the LDS copy of the header bytes.
 FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const ffcv_sample &smp,
                           const JpegArgs &a, int k, int MODE) {
-  auto B = [&](uint32_t p) -> int { return p < HDR_BYTES ? S.u.hdr[p] : src[p]; };
+  auto B = [&](uint32_t p) -> int {
+    int v;
+    if (p < HDR_BYTES)
+      v = S.u.hdr[p];
+    else
+      v = __builtin_nontemporal_load(src + p);
+    return v;
+  };
   auto R16 = [&](uint32_t p) -> int { return (B(p) << 8) | B(p + 1); };
   for (int i = 0; i < 4; i++) S.dqt_ok[i] = 0;
   for (int i = 0; i < NTAB; i++) S.dht_ok[i] = 0;
@@ -577,9 +632,39 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
       }
       if (nb > 10) return FFCV_SAMPLE_UNSUPPORTED;
       S.bpm = nb;
+      // table slots: AC tables first (they decode most symbols), so they
+      // always get a fast LUT
+      S.nslots = 0;
+      S.dcpack = S.acpack = S.acmask = 0;
+      for (int pass = 0; pass < 2; pass++) {
+        for (int b = 0; b < nb; b++) {
+          int c = S.blk_comp[b];
+          int tab = pass == 0 ? 4 + S.ta[c] : S.td[c];
+          int sl = -1;
+          for (int q = 0; q < S.nslots; q++)
+            if (S.slot_tab[q] == tab) sl = q;
+          if (sl < 0) {
+            sl = S.nslots++;
+            S.slot_tab[sl] = tab;
+            if (pass == 0) S.acmask |= 1u << sl;
+          }
+          if (pass == 0)
+            S.acpack |= (uint32_t)sl << (3 * b);
+          else
+            S.dcpack |= (uint32_t)sl << (3 * b);
+        }
+      }
+      // first-level LUT space from the pool, in slot order (AC slots first)
+      uint32_t used = 0;
+      for (int q = 0; q < S.nslots; q++) {
+        uint32_t bits = S.slot_tab[q] >= 4 ? FB_AC : FB_DC;
+        if (used + (1u << bits) > LUT_POOL) bits = 0;  // canonical decode only
+        S.sinfo[q] = (bits ? used : 0u) | (bits << 16) | ((uint32_t)q << 20);
+        used += bits ? (1u << bits) : 0u;
+      }
       for (int b = 0; b < nb; b++) {
-        S.ph_dc[b] = S.td[S.blk_comp[b]];
-        S.ph_ac[b] = 4 + S.ta[S.blk_comp[b]];
+        S.dinf[b] = S.sinfo[slot_of(S.dcpack, b)];
+        S.ainf[b] = S.sinfo[slot_of(S.acpack, b)];
       }
       S.scan_off = p + (uint32_t)len;
       have_sos = 1;
@@ -664,6 +749,16 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     S.wx0[c] = x0 >> 3;
     S.wx1[c] = x1 >> 3;
   }
+  for (int b = 0; b < S.bpm; b++) {
+    int c = S.blk_comp[b], dx = S.blk_dx[b], dy = S.blk_dy[b], hs = S.hs[c], vs = S.vs[c];
+    // bx = mx * hs + dx in [wx0, wx1]  <=>  mx in [mx_lo, mx_hi]
+    int mxl = S.wx0[c] - dx <= 0 ? 0 : (S.wx0[c] - dx + hs - 1) / hs;
+    int mxh = S.wx1[c] - dx < 0 ? -1 : (S.wx1[c] - dx) / hs;
+    int myl = S.wy0[c] - dy <= 0 ? 0 : (S.wy0[c] - dy + vs - 1) / vs;
+    int myh = S.wy1[c] - dy < 0 ? -1 : (S.wy1[c] - dy) / vs;
+    S.pdesc[b][0] = make_int4((int)(S.coff[c] + (uint64_t)dy * S.bw[c] + dx), vs * S.bw[c], hs, mxl);
+    S.pdesc[b][1] = make_int4(mxh, myl, myh, 0);
+  }
   return FFCV_SAMPLE_OK;
 }
 
@@ -683,18 +778,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
   }
   const uint8_t *src = a.base + smp.offset;
   const uint32_t nbytes = (uint32_t)smp.size;
-
-  // ------------------------------------------------------------- P0 ----
-  STAMP(0);
-  for (uint32_t i = t; i < HDR_BYTES; i += JT) S.u.hdr[i] = i < nbytes ? src[i] : 0;
-  __syncthreads();
-  if (t == 0) {
-    S.status = parse_header(S, src, nbytes, smp, a, k, MODE);
-    S.first_marker = 0xFFFFFFFFu;
-    S.any = 0;
-  }
-  __syncthreads();
-  if (S.status != FFCV_SAMPLE_OK) {
+  auto fail = [&]() {
     if (t == 0) {
       a.status[k] = S.status;
       info->status = S.status;
@@ -704,32 +788,73 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
       uint8_t *o = (uint8_t *)a.out + a.out_stride * k;
       for (uint64_t i = t; i < bytes && i < a.out_stride; i += JT) o[i] = 0;
     }
+  };
+
+  // ------------------------------------------------------------- P0 ----
+  STAMP(0);
+  {
+    // aligned dword loads (one batch per lane), bytes scattered into LDS
+    const uint32_t nh = min(nbytes, (uint32_t)HDR_BYTES);
+    const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
+    const uint32_t *aw = (const uint32_t *)(src - mis);
+    constexpr int NW = (HDR_BYTES + 4) / 4;
+#pragma unroll
+    for (int r = 0; r < (NW + JT - 1) / JT; r++) {
+      const int i = r * JT + t;
+      const int b0 = 4 * i - (int)mis;
+      const uint32_t w = i < NW && b0 < (int)nh ? __builtin_nontemporal_load(aw + i) : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int idx = b0 + j;
+        if (idx >= 0 && idx < HDR_BYTES) S.u.hdr[idx] = idx < (int)nh ? (uint8_t)(w >> (8 * j)) : 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    S.status = parse_header(S, src, nbytes, smp, a, k, MODE);
+    S.any = 0;
+  }
+  __syncthreads();
+  if (S.status != FFCV_SAMPLE_OK) {
+    fail();
     return;
   }
 
   // ------------------------------------------------------------- P1 ----
   STAMP(1);
-  auto HB = [&](uint32_t p) -> int { return p < HDR_BYTES ? S.u.hdr[p] : src[p]; };
-  if (t < NTAB && S.dht_ok[t]) {
-    uint32_t d = S.dht_off[t];
-    int code = 0, kk = 0;
+  auto HB = [&](uint32_t p) -> int {
+    int v;
+    if (p < HDR_BYTES)
+      v = S.u.hdr[p];
+    else
+      v = __builtin_nontemporal_load(src + p);
+    return v;
+  };
+  if (t < S.nslots) {
+    // jdhuff.c jpeg_make_d_derived_tbl, including its table checks
+    const int tab = S.slot_tab[t];
+    const uint32_t d = S.dht_off[tab];
+    uint32_t code = 0;
+    int kk = 0;
+    bool bad = false;
     for (int l = 1; l <= 16; l++) {
       int nl = HB(d + l - 1);
-      if (nl) {
-        S.valoff[t][l] = kk - code;
-        code += nl;
-        kk += nl;
-        S.maxcode[t][l] = code - 1;
-      } else {
-        S.maxcode[t][l] = -1;
-        S.valoff[t][l] = 0;
-      }
+      S.valoff[t][l] = kk - (int)code;
+      code += nl;
+      kk += nl;
+      if (code >= (1u << l)) bad = true;  // over-subscribed (or all-ones) code space
+      S.lim[t][l] = code << (16 - l);
       code <<= 1;
     }
-    S.maxcode[t][17] = 0x7fffffff;
-    for (int i = 0; i < kk; i++) S.vals[t][i] = (uint8_t)HB(d + 16 + i);
+    for (int i = 0; i < kk; i++) {
+      int v = HB(d + 16 + i);
+      if (tab < 4 && v > 15) bad = true;  // DC sizes are 0..15
+      S.vals[t][i] = (uint8_t)v;
+    }
+    if (bad) S.status = FFCV_SAMPLE_BAD_MARKER;
+    S.nsub[t] = 0;
   }
-  if (t < 80) S.nat[t] = c_natural[t];
   for (int i = t; i < S.ncomp * 64; i += JT) {
     int c = i >> 6, zz = i & 63;
     int tq = S.tq[c];
@@ -738,79 +863,119 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     int n = c_natural[zz];
     S.qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
   }
-  __syncthreads();
-  for (int i = t; i < NTAB * (1 << FAST_BITS); i += JT) {
-    int ti = i >> FAST_BITS, v = i & ((1 << FAST_BITS) - 1);
-    if (!S.dht_ok[ti]) continue;
-    uint16_t e = 0;
-    for (int l = 1; l <= FAST_BITS; l++) {
-      int code = v >> (FAST_BITS - l);
-      if (code <= S.maxcode[ti][l]) {
-        e = (uint16_t)((l << 8) | S.vals[ti][(S.valoff[ti][l] + code) & 0xff]);
-        break;
-      }
-    }
-    S.lut[ti][v] = e;
+  __syncthreads();  // header bytes are dead from here (the LUT pool reuses them)
+  if (S.status != FFCV_SAMPLE_OK) {
+    fail();
+    return;
   }
-  // zero the coefficient blocks of the window (P5 writes only nonzeros)
-  int16_t *coef = a.coef + a.coef_slot * k;
-  for (int c = 0; c < S.ncomp; c++) {
-    int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
-    int n16 = wbw * wbh * 8;
-    for (int i = t; i < n16; i += JT) {
-      int blk = i >> 3, piece = i & 7;
-      int by = S.wy0[c] + blk / wbw, bx = S.wx0[c] + blk % wbw;
-      *(uint4 *)(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64 + piece * 8) = make_uint4(0, 0, 0, 0);
-    }
-  }
-  __syncthreads();  // header bytes are dead from here (the stream reuses them)
-
-  // ------------------------------------------------------------- P2 ----
-  STAMP(2);
-  const uint32_t seg0 = S.scan_off;
-  const uint32_t seglen = nbytes > seg0 ? nbytes - seg0 : 0;
-  const uint32_t per = (seglen + JT - 1) / JT;
-  const uint32_t c0 = seg0 + min(seglen, per * t), c1 = seg0 + min(seglen, per * (t + 1));
-  uint32_t keep_all = 0, keep_before = 0, fm = 0xFFFFFFFFu;
-  {
-    int prev = c0 > seg0 ? src[c0 - 1] : 0;
-    for (uint32_t q = c0; q < c1; q++) {
-      int b = src[q];
-      if (b == 0xFF && fm == 0xFFFFFFFFu) {
-        int nx = q + 1 < nbytes ? src[q + 1] : 0xD9;
-        if (nx != 0x00) {
-          fm = q;
-          keep_before = keep_all;
+  const int nslots = S.nslots;
+  for (int s = 0; s < nslots; s++) {
+    const uint32_t inf = S.sinfo[s];
+    const int bits = (int)((inf >> 16) & 15);
+    if (!bits) continue;
+    const bool ac = (S.acmask >> s) & 1;
+    for (int v = t; v < (1 << bits); v += JT) {
+      const uint32_t look = (uint32_t)v << (16 - bits);
+      int len = 1;
+      for (int l = 1; l < bits; l++) len += look >= S.lim[s][l];
+      uint32_t e = 0;
+      if (look < S.lim[s][len]) {
+        int sym = S.vals[s][(S.valoff[s][len] + (int)(look >> (16 - len))) & 0xff];
+        e = make_entry(ac, len, sym);
+      } else if (look < S.lim[s][16]) {  // codes longer than `bits` under this prefix
+        int n = atomicAdd(&S.nsub[s], 1);
+        if (n < NSUB) {
+          S.sub_prefix[s][n] = (uint16_t)v;
+          e = 0x8000u | (uint32_t)n;
         }
       }
-      keep_all += !(b == 0x00 && prev == 0xFF && q > seg0);
-      prev = b;
+      S.u.lut[(inf & 0xffff) + v] = (uint16_t)e;
     }
-    if (fm != 0xFFFFFFFFu) atomicMin(&S.first_marker, fm);
   }
   __syncthreads();
-  const uint32_t seg_end = S.first_marker == 0xFFFFFFFFu ? nbytes : S.first_marker;
-  uint32_t keep = c1 <= seg_end ? keep_all : (c0 >= seg_end ? 0u : keep_before);
-  uint32_t wpos = wg_exscan_u32(keep, S.scan_tmp);
-  if (t == JT - 1) S.dlen = wpos + keep;
-  __syncthreads();
-  const uint32_t dlen = S.dlen;
-  const bool in_lds = dlen + 16 <= LDS_STREAM_BYTES;
+  for (int i = t; i < NSLOT * NSUB * (1 << SUBB); i += JT) {
+    const int s = i / (NSUB << SUBB), n = (i >> SUBB) % NSUB, x = i & ((1 << SUBB) - 1);
+    if (s >= nslots || n >= min(S.nsub[s], NSUB)) continue;
+    const int bits = (int)((S.sinfo[s] >> 16) & 15);
+    const uint32_t look = ((uint32_t)S.sub_prefix[s][n] << (16 - bits)) | ((uint32_t)x << (16 - bits - SUBB));
+    int len = 1;
+    for (int l = 1; l < 16; l++) len += look >= S.lim[s][l];
+    S.lut2[s][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(S, s, look) : (uint16_t)0;
+  }
+  // the coefficient slot is all zeros here: the IDCT kernel zeroes every
+  // block it consumes (and ffcv_jpeg_create zeroed the slot)
+  int16_t *coef = a.coef + a.coef_slot * k;
+
+  // ------------------------------------------------------------- P2 ----
+  // De-stuffing in stream order: each step the wave reads 64 consecutive
+  // aligned dwords of the segment (one per lane), keeps every byte except a
+  // 0x00 after 0xFF, stops at the first marker (0xFF + non-zero), and
+  // writes the kept bytes at offsets from a wave scan of their counts.
+  STAMP(2);
   uint8_t *gds = a.dstuff + a.dstuff_slot * k;
-  uint8_t *dsb = in_lds ? (uint8_t *)S.u.stream : gds;
+  uint32_t dlen = 0;
   {
-    uint32_t end = min(c1, seg_end);
-    int prev = c0 > seg0 ? src[c0 - 1] : 0;
-    for (uint32_t q = c0; q < end; q++) {
-      int b = src[q];
-      if (!(b == 0x00 && prev == 0xFF && q > seg0)) dsb[wpos++] = (uint8_t)b;
-      prev = b;
+    const uint32_t seg0 = S.scan_off;
+    const uint32_t seglen = nbytes > seg0 ? nbytes - seg0 : 0;
+    const uintptr_t sb = (uintptr_t)(src + seg0);
+    const uint32_t mis = (uint32_t)(sb & 3);
+    const uint32_t *aw = (const uint32_t *)(sb - mis);
+    const uint32_t ndw = (seglen + mis + 3) / 4;
+    uint32_t carry = 0;  // byte before this step's first byte (0: none / not 0xFF)
+    // 4-deep prefetch ring: step i works on r0 while steps i+1..i+3 load
+    auto ld = [&](uint32_t d) -> uint32_t { return d < ndw ? __builtin_nontemporal_load(aw + d) : 0u; };
+    uint32_t r0 = ld(t), r1 = ld(JT + t), r2 = ld(2 * JT + t), r3 = ld(3 * JT + t);
+    for (uint32_t base = 0; base < ndw; base += JT) {
+      const uint32_t di = base + t;
+      const uint32_t w = r0;
+      r0 = r1;
+      r1 = r2;
+      r2 = r3;
+      r3 = ld(base + 4 * JT + t);
+      const uint32_t wprev = __shfl_up(w, 1);
+      const uint32_t wnext = __shfl_down(w, 1);
+      const uint32_t nfirst = __shfl(r0, 0);  // next step's first dword
+      const uint32_t prevb = t == 0 ? carry : (wprev >> 24);
+      const uint32_t next0 = (t == JT - 1 ? nfirst : wnext) & 0xff;
+      int first_mk = 4;  // first marker byte index in this dword
+      uint32_t keepm = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int rel = (int)(4 * di + j) - (int)mis;
+        const bool valid = rel >= 0 && rel < (int)seglen;
+        const uint32_t b = (w >> (8 * j)) & 0xff;
+        const uint32_t pb = j == 0 ? prevb : (w >> (8 * j - 8)) & 0xff;
+        uint32_t nx = j == 3 ? next0 : (w >> (8 * j + 8)) & 0xff;
+        nx = rel + 1 < (int)seglen ? nx : 0xD9u;  // end of data acts as a marker
+        const bool removed = rel > 0 && b == 0 && pb == 0xFF;
+        const bool marker = valid && b == 0xFF && nx != 0;
+        if (marker && first_mk == 4) first_mk = j;
+        if (valid && !removed) keepm |= 1u << j;
+      }
+      // the first marker of the step ends the segment
+      const uint64_t mk = __ballot(first_mk < 4);
+      bool stop = false;
+      if (mk) {
+        const int ml = __ffsll((unsigned long long)mk) - 1;
+        const int mj = __shfl(first_mk, ml);
+        if (t > ml) keepm = 0;
+        if (t == ml) keepm &= (1u << mj) - 1;
+        stop = true;
+      }
+      const uint32_t cnt = __popc(keepm);
+      uint32_t off = dlen + wave_exscan(cnt);
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (keepm & (1u << j)) gds[off++] = (uint8_t)(w >> (8 * j));
+      dlen = __shfl(off, JT - 1);
+      carry = __shfl(w, JT - 1) >> 24;
+      if (stop) break;
     }
   }
+  if (t < STREAM_PAD) gds[dlen + t] = 0;  // zero fill, as libjpeg past a marker
+  __threadfence_block();
   __syncthreads();
-  if (t < 16) dsb[dlen + t] = 0;  // zero fill, as libjpeg past a marker
-  __syncthreads();
-  const uint32_t nwords = (dlen + 3) / 4;
+  const uint32_t *words = (const uint32_t *)gds;
   const uint32_t total_bits = dlen * 8;
 
   // ------------------------------------------------------------- P3 ----
@@ -825,101 +990,97 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
   g.z = 0;
   g.ph = 0;
   uint32_t my_cnt = 0;
+  int my_nev = 0, my_cb = 0;
   DecState e = g;
-  S.nev[t] = 0;
-  LdsWords lw{S.u.stream, nwords};
-  GlobalWords gw{(const uint32_t *)gds, nwords};
-  if (active) {
-    if (in_lds)
-      e = sync_range(S, lw, g, my_end, t, &my_cnt, g, 0, -1);
-    else
-      e = sync_range(S, gw, g, my_end, t, &my_cnt, g, 0, -1);
-  }
+  uint32_t it_lane = 0, it_wave = 0;  // diagnostics: loop iterations (max over lanes per round)
+  if (active) e = sync_range(S, words, g, my_end, t, my_cnt, my_nev, my_cb, g, false, it_lane);
+  if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
   int rounds = 0;
   for (;;) {
-    S.e_pos[t] = e.pos;
-    S.e_zph[t] = (uint16_t)(e.z | (e.ph << 8));
-    __syncthreads();
-    bool changed = false;
-    DecState ng = g;
-    if (active && t > 0) {
-      ng.pos = S.e_pos[t - 1];
-      ng.z = S.e_zph[t - 1] & 0xff;
-      ng.ph = S.e_zph[t - 1] >> 8;
-      changed = ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph;
-    }
-    int anyc = __syncthreads_or(changed);
-    if (!anyc) break;
+    DecState ng;
+    ng.pos = __shfl_up(e.pos, 1);
+    ng.z = __shfl_up(e.z, 1);
+    ng.ph = __shfl_up(e.ph, 1);
+    const bool changed = active && t > 0 && (ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph);
+    if (!__any(changed)) break;
     rounds++;
     if (changed) {
       g = ng;
       if (g.pos >= my_end) {
         e = g;
         my_cnt = 0;
-        S.nev[t] = 0;
+        my_nev = 0;
       } else {
-        int onev = S.nev[t];
-        uint32_t ocnt = my_cnt;
-        if (in_lds)
-          e = sync_range(S, lw, g, my_end, t, &my_cnt, e, ocnt, onev);
-        else
-          e = sync_range(S, gw, g, my_end, t, &my_cnt, e, ocnt, onev);
+        it_lane = 0;
+        e = sync_range(S, words, g, my_end, t, my_cnt, my_nev, my_cb, e, true, it_lane);
       }
     }
+    if (a.dbg) it_wave += __reduce_max_sync(~0ull, changed ? it_lane : 0u);
   }
   if (!active) my_cnt = 0;
   if (a.dbg && t == 0) {
     a.dbg[(uint64_t)k * 16 + 12] = (uint64_t)rounds;
     a.dbg[(uint64_t)k * 16 + 13] = (uint64_t)nthr;
+    a.dbg[(uint64_t)k * 16 + 14] = (uint64_t)it_wave;
   }
 
   // ------------------------------------------------------------- P4 ----
   STAMP(4);
-  const uint32_t blk_base = wg_exscan_u32(my_cnt, S.scan_tmp);
+  const uint32_t blk_base = wave_exscan(my_cnt);
+  bool bad_lane = false;
   if (active) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur < 0 || (cur % S.bpm) != g.ph) S.any = 1;  // inconsistent stream
+    bad_lane = cur < 0 || (cur % S.bpm) != g.ph;  // inconsistent stream
   }
+  const bool any_bad = __any(bad_lane);
 
   // ------------------------------------------------------------- P5 ----
   STAMP(5);
   int16_t *dcd = a.dcd + a.dcd_slot * k;
+  uint32_t it_lane2 = 0;
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur >= 0) {
-      if (in_lds)
-        write_range(S, lw, g, my_end, cur, coef, dcd);
-      else
-        write_range(S, gw, g, my_end, cur, coef, dcd);
-    }
+    if (cur >= 0) write_range(S, words, g, my_end, cur, coef, dcd, it_lane2);
   }
+  if (a.dbg) {
+    const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
+    if (t == 0) a.dbg[(uint64_t)k * 16 + 15] = (uint64_t)wmax;
+  }
+  __threadfence_block();
   __syncthreads();
 
   // ------------------------------------------------------------- P6 ----
   // DC prediction (jdhuff.c last_dc_val): per-component running sum of DC
-  // differences in MCU block order, as a workgroup scan over block ranges.
+  // differences in MCU block order, as a wave scan over block ranges.
   STAMP(6);
   {
     const int nb = S.nblocks;
     const int per_b = (nb + JT - 1) / JT;
     const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
-    int32_t sum[3] = {0, 0, 0};
+    int32_t s0 = 0, s1 = 0, s2 = 0;  // (registers: no dynamically indexed arrays)
     int ph = b0 % S.bpm;
     for (int b = b0; b < b1; b++) {
-      sum[S.blk_comp[ph]] += dcd[b];
+      const int c = S.blk_comp[ph];
+      const int d = dcd[b];
+      s0 += c == 0 ? d : 0;
+      s1 += c == 1 ? d : 0;
+      s2 += c == 2 ? d : 0;
       if (++ph == S.bpm) ph = 0;
     }
-    int32_t pred[3] = {sum[0], sum[1], sum[2]};
-    wg_exscan3(pred, S.scan3);
+    int32_t p0 = wave_exscan_i(s0), p1 = wave_exscan_i(s1), p2 = wave_exscan_i(s2);
     ph = b0 % S.bpm;
     int m = b0 / S.bpm;
     int my = m / S.mcux, mx = m - my * S.mcux;
     for (int b = b0; b < b1; b++) {
-      int c = S.blk_comp[ph];
-      pred[c] += dcd[b];
+      const int c = S.blk_comp[ph];
+      const int d = dcd[b];
+      p0 += c == 0 ? d : 0;
+      p1 += c == 1 ? d : 0;
+      p2 += c == 2 ? d : 0;
+      const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
       int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
       if (bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c])
-        coef[(S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64] = (int16_t)pred[c];
+        coef[(S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64] = (int16_t)pv;
       if (++ph == S.bpm) {
         ph = 0;
         if (++mx == S.mcux) {
@@ -929,6 +1090,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
       }
     }
   }
+  __threadfence_block();
   __syncthreads();
 
   if (MODE == JM_COEF) {
@@ -939,29 +1101,26 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
       int my = (int)(m / S.mcux), mx = (int)(m - (int64_t)my * S.mcux);
       int c = S.blk_comp[ph];
       int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
-      const uint4 *sp = (const uint4 *)(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64);
+      const int16_t *cp = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
+      int16_t zz[64], nb[64];
+#pragma unroll
+      for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
+#pragma unroll
+      for (int n = 0; n < 64; n++) nb[n] = zz[kZigzagOfNatural[n]];
       uint4 *dp = (uint4 *)(o + b * 64);
-      for (int i = 0; i < 8; i++) dp[i] = sp[i];
+#pragma unroll
+      for (int p8 = 0; p8 < 8; p8++) dp[p8] = *(const uint4 *)(nb + p8 * 8);
+#pragma unroll
+      for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);  // slot back to zeros
     }
-    if (t == 0) a.status[k] = S.any ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
+    if (t == 0) a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
     return;
   }
 
   // ------------------------------------------------------------- P7 ----
+  // geometry + window + multipliers for jpeg_idct_kernel and K2
   STAMP(7);
-  uint8_t *planes = a.planes + a.plane_slot * k;
-  for (int c = 0; c < S.ncomp; c++) {
-    int wbw = S.wx1[c] - S.wx0[c] + 1, wbh = S.wy1[c] - S.wy0[c] + 1;
-    int stride = S.bw[c] * 8;
-    for (int i = t; i < wbw * wbh; i += JT) {
-      int by = S.wy0[c] + i / wbw, bx = S.wx0[c] + i % wbw;
-      const int16_t *cp = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
-      int16_t blk[64];
-#pragma unroll
-      for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(blk + p8 * 8) = ((const uint4 *)cp)[p8];
-      idct_ifast_block(blk, S.qmul[c], planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
-    }
-  }
+  for (int i = t; i < 3 * 64; i += JT) info->qmul[i >> 6][i & 63] = (i >> 6) < S.ncomp ? S.qmul[i >> 6][i & 63] : 0;
   if (t == 0) {
     info->status = FFCV_SAMPLE_OK;
     info->W = S.W;
@@ -976,14 +1135,57 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
       info->ch[c] = v ? S.ch[c] : 0;
       info->stride[c] = v ? S.bw[c] * 8 : 0;
       info->poff[c] = v ? S.poff[c] : 0;
+      info->wx0[c] = v ? S.wx0[c] : 0;
+      info->wy0[c] = v ? S.wy0[c] : 0;
+      info->wbw[c] = v ? S.wx1[c] - S.wx0[c] + 1 : 0;
+      info->wbh[c] = v ? S.wy1[c] - S.wy0[c] + 1 : 0;
+      info->bw[c] = v ? S.bw[c] : 0;
+      info->coff[c] = v ? S.coff[c] : 0;
     }
     info->ri = S.ri;
     info->rj = S.rj;
     info->rh = S.rh;
     info->rw = S.rw;
-    a.status[k] = S.any ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
+    a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
   }
   STAMP(8);
+}
+
+// ======================================================================= //
+// K1b: de-zigzag + dequantise + ifast IDCT of every window block, one      //
+// thread per block over the whole batch; each block is zeroed after it is  //
+// read, which keeps the coefficient slot all-zero for the next batch.      //
+// ======================================================================= //
+#define IDCT_T 256
+__global__ void __launch_bounds__(IDCT_T) jpeg_idct_kernel(JpegArgs a) {
+  const int k = blockIdx.y;
+  const ImgInfo *I = a.info + k;
+  if (I->status != FFCV_SAMPLE_OK) return;
+  int i = blockIdx.x * IDCT_T + threadIdx.x;
+  const int n0 = I->wbw[0] * I->wbh[0], n1 = I->wbw[1] * I->wbh[1], n2 = I->wbw[2] * I->wbh[2];
+  if (i >= n0 + n1 + n2) return;
+  int c = 0;
+  if (i >= n0) {
+    i -= n0;
+    c = 1;
+    if (i >= n1) {
+      i -= n1;
+      c = 2;
+    }
+  }
+  const int wbw = I->wbw[c];
+  const int by = I->wy0[c] + i / wbw, bx = I->wx0[c] + i % wbw;
+  int16_t *cp = a.coef + a.coef_slot * k + (I->coff[c] + (uint64_t)by * I->bw[c] + bx) * 64;
+  int16_t zz[64], blk[64];
+#pragma unroll
+  for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
+#pragma unroll
+  for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int n = 0; n < 64; n++) blk[n] = zz[kZigzagOfNatural[n]];
+  const int stride = I->stride[c];
+  idct_ifast_block(blk, I->qmul[c], a.planes + a.plane_slot * k + I->poff[c] + (uint64_t)by * 8 * stride + bx * 8,
+                   stride);
 }
 
 // ======================================================================= //
@@ -1136,7 +1338,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   // Bands too wide for LDS stage their rows in the image's coefficient slot
   // (dead once K1 has run) at their absolute crop-row position; rows shared
   // with a neighbouring band are written with identical bytes by both.
-  uint8_t *groi = (uint8_t *)(a.coef + a.coef_slot * k);
+  uint8_t *groi = a.rgb + a.plane_slot * k;
   uint8_t *dst = staged ? roi : groi + (uint64_t)r0 * step;
   for (int i = t; i < nrows * I.rw; i += K2T) {
     int yy = i / I.rw, x = i - yy * I.rw;
@@ -1203,7 +1405,9 @@ struct ffcv_jpeg_ctx {
   uint64_t plane_slot;
   int16_t *dcd;
   uint64_t dcd_slot;
+  uint8_t *rgb;  // K2 band staging when a band's source rows exceed LDS
   ImgInfo *info;
+  uint64_t nblk;
 };
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -1213,6 +1417,7 @@ static void free_ctx(ffcv_jpeg_ctx *c) {
   (void)hipFree(c->coef);
   (void)hipFree(c->planes);
   (void)hipFree(c->dcd);
+  (void)hipFree(c->rgb);
   (void)hipFree(c->info);
   delete c;
 }
@@ -1237,12 +1442,17 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
   c->coef_slot = align_up(nblk * 64, 128);   // int16 elements
   c->plane_slot = align_up(nblk * 64, 256);  // bytes
   c->dcd_slot = align_up(nblk, 128);         // int16 elements
+  c->nblk = nblk;
   hipError_t e;
   if ((e = hipMalloc(&c->dstuff, c->dstuff_slot * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->coef, c->coef_slot * 2 * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->planes, c->plane_slot * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->dcd, c->dcd_slot * 2 * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess) {
+      (e = hipMalloc(&c->rgb, c->plane_slot * max_batch)) != hipSuccess ||
+      (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
+      // the entropy kernel writes only non-zero coefficients into an
+      // all-zero slot; the IDCT kernel restores the zeros it consumed
+      (e = hipMemset(c->coef, 0, c->coef_slot * 2 * max_batch)) != hipSuccess) {
     int rc = ffcv::check_hip(e, "ffcv_jpeg_create: hipMalloc");
     free_ctx(c);
     return rc;
@@ -1277,6 +1487,7 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.plane_slot = c->plane_slot;
   a.dcd = c->dcd;
   a.dcd_slot = c->dcd_slot;
+  a.rgb = c->rgb;
   a.info = c->info;
   a.max_h = c->max_h;
   a.max_w = c->max_w;
@@ -1319,6 +1530,8 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   hipStream_t s = ffcv::as_stream(stream);
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3(batch), dim3(JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
+  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (fp16)
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, true>), g2, dim3(K2T), K2_LDS, s, a);
@@ -1343,6 +1556,8 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   hipStream_t s = ffcv::as_stream(stream);
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3(batch), dim3(JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
+  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
   dim3 g2((c->max_h + BAND - 1) / BAND, batch);
   hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_FULL, false>), g2, dim3(K2T), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<FULL>");

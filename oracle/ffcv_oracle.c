@@ -465,6 +465,7 @@ typedef struct {
   uint8_t bits[17];
   uint8_t vals[256];
   int32_t mincode[17], maxcode[18], valptr[17];
+  int bad; /* jdhuff.c jpeg_make_d_derived_tbl would reject it */
 } huff_t;
 
 typedef struct {
@@ -479,8 +480,12 @@ typedef struct {
   int scan_comp[4];
 } jdec_t;
 
-static void huff_build(huff_t *h) {
+/* jdhuff.c jpeg_make_d_derived_tbl: canonical codes; a length whose codes
+ * reach 2^l (over-subscribed or all-ones code) and, for DC tables, a symbol
+ * above 15 are JERR_BAD_HUFF_TABLE (checked for the tables a scan uses). */
+static void huff_build(huff_t *h, int is_dc) {
   int code = 0, k = 0;
+  h->bad = 0;
   for (int l = 1; l <= 16; l++) {
     if (h->bits[l]) {
       h->valptr[l] = k;
@@ -491,9 +496,13 @@ static void huff_build(huff_t *h) {
     } else {
       h->maxcode[l] = -1;
     }
+    if (code >= (1 << l)) h->bad = 1;
     code <<= 1;
   }
   h->maxcode[17] = 0x7fffffff;
+  if (is_dc)
+    for (int i = 0; i < k; i++)
+      if (h->vals[i] > 15) h->bad = 1;
 }
 
 static int rd16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
@@ -547,7 +556,7 @@ static int jpeg_parse(const uint8_t *buf, size_t n, jdec_t *d) {
         memcpy(h->vals, s + o, (size_t)total);
         o += total;
         h->present = 1;
-        huff_build(h);
+        huff_build(h, tc == 0);
       }
     } else if (m == 0xC0 || m == 0xC1) { /* baseline / extended sequential */
       if (s[0] != 8) return -6;
@@ -615,6 +624,7 @@ static int jpeg_parse(const uint8_t *buf, size_t n, jdec_t *d) {
       for (int c = 0; c < in->ncomp; c++) {
         if (!d->qt_present[in->tq[c]]) return -13;
         if (!d->dc[in->td[c]].present || !d->ac[in->ta[c]].present) return -14;
+        if (d->dc[in->td[c]].bad || d->ac[in->ta[c]].bad) return -5;
       }
       return 0;
     }

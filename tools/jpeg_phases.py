@@ -49,3 +49,4 @@ print('span of K1 us', (d[:, 8].max() - d[:, 0].min()) / 100.0)
 print('rounds hist', np.bincount(d[:, 12].astype(int))[:20], 'nthr mean', d[:, 13].mean())
 st = (d[:, 0] - d[:, 0].min()) / 100.0
 print('start offsets us: p50', np.median(st), 'max', st.max())
+print('sync wave-iterations mean', d[:, 14].mean(), 'max', d[:, 14].max(), '| write wave-iterations mean', d[:, 15].mean(), 'max', d[:, 15].max())

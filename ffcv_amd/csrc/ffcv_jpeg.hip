@@ -55,14 +55,18 @@
 
 #define JT 64           // lanes per image (one wave)
 #define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
-#define LUT_POOL 6144   // first-level LUT entries shared by the slots
+#define LUT_POOL 5121   // first-level LUT words shared by the slots (+ the zero word)
 #define FB_AC 11        // first-level bits, AC tables
 #define FB_DC 9         // first-level bits, DC tables
 #define SUBB 5          // second-level bits
 #define NSUB 8          // second-level tables per slot
 #define NSLOT 6         // Huffman tables a scan can reference (3 DC + 3 AC)
+#define NLUTSLOT 4      // slots that can get a first-level LUT from the pool
 #define NTAB 8
-#define NEV 10
+#define NEV 8
+#define DS_FLUSH 16     // de-stuff steps per LDS -> HBM flush
+#define DS_DEPTH 8      // de-stuff loads in flight per lane
+#define STAGE_DUMMY (2 * (NEV + 1) * JT * 4 - 4)
 #define STREAM_PAD 32   // zero bytes after the de-stuffed stream
 #define BAND 16
 #define K2T 256
@@ -97,7 +101,7 @@ struct JShared {
   // slot numbers packed 3 bits per phase; per slot LUT base and bits
   int nslots;
   int slot_tab[NSLOT];  // class * 4 + id
-  uint32_t sinfo[NSLOT];  // base | bits << 16 | slot << 20
+  uint32_t sinfo[NSLOT];  // base | bits << 16 | slot << 20 | second-level set << 23
   uint32_t dinf[10], ainf[10];  // sinfo of each block-in-MCU's DC / AC table
   uint32_t dcpack, acpack, acmask;
   uint32_t scan_off;
@@ -121,14 +125,15 @@ struct JShared {
   uint32_t lim[NSLOT][17];  // left-justified end of length-l codes
   int32_t valoff[NSLOT][17];
   uint8_t vals[NSLOT][256];
-  int16_t qmul[3][64];
   int nsub[NSLOT];
+  int nvals[NSLOT];
   uint16_t sub_prefix[NSLOT][NSUB];
-  // decode entry: (len-1) | size << 4 | zinc << 8; 0x8000 | n = second-level
-  // table n; 0 = canonical slow path
-  uint16_t lut2[NSLOT][NSUB][1 << SUBB];
-  int32_t scan3[3][JT];
-  uint32_t ev[2][NEV + 1][JT];  // block-start events (pos << 4 | phase), double-buffered
+  // second-level tables (codes longer than the first level; make_entry format)
+  uint16_t lut2[NLUTSLOT][NSUB][1 << SUBB];
+  union {
+    uint32_t ev[2][NEV + 1][JT];  // P3: block-start events (pos << 4 | phase), double-buffered
+    uint8_t stage[2 * (NEV + 1) * JT * 4];  // P2: de-stuffed bytes awaiting a flush
+  };
   // header bytes, then the first-level LUT pool (same storage)
   union {
     uint8_t hdr[HDR_BYTES];
@@ -197,8 +202,11 @@ struct DecState {
   int ph;  // block index inside the MCU
 };
 
-// Symbol -> decode entry.  DC: size = symbol, z 0 -> 1.  AC: size = low
-// nibble; z advances by run+1, by 16 for ZRL, past the block for EOB.
+// Symbol -> decode entry: bits consumed (code + extra bits, 1..31) | extra
+// bits << 5 | coefficient advance << 9.  DC: size = symbol, z 0 -> 1.  AC:
+// size = low nibble; z advances by run+1, by 16 for ZRL, past the block for
+// EOB.  A LUT word with bits-consumed 0 is not an entry: 0 sends the decode
+// to the canonical fallback, (n + 1) << 5 to second-level table n.
 FFCV_DEV uint32_t make_entry(bool ac, int len, int sym) {
   int size, zinc;
   if (!ac) {
@@ -209,7 +217,7 @@ FFCV_DEV uint32_t make_entry(bool ac, int len, int sym) {
     int r = sym >> 4;
     zinc = size ? r + 1 : (r == 15 ? 16 : 127);
   }
-  return (uint32_t)(len - 1) | ((uint32_t)size << 4) | ((uint32_t)zinc << 8);
+  return (uint32_t)(len + size) | ((uint32_t)size << 5) | ((uint32_t)zinc << 9);
 }
 
 // Canonical decode of a 16-bit lookahead (jdhuff.c jpeg_huff_decode): the
@@ -225,14 +233,17 @@ FFCV_DEV uint32_t slow_entry(const JShared &S, int slot, uint32_t look) {
   return make_entry((S.acmask >> slot) & 1, len, sym);
 }
 
-// inf = sinfo of the table: LUT base | bits << 16 | slot << 20 (bits 0: none)
+// inf = sinfo of the table: LUT base | bits << 16 | slot << 20 | second-
+// level set << 23.  A slot without a first-level LUT (bits 0) points at a
+// reserved zero word.
 FFCV_DEV uint32_t decode_entry(const JShared &S, uint32_t inf, uint64_t acc) {
   const uint32_t look = (uint32_t)(acc >> 48);
-  const int bits = (int)((inf >> 16) & 15), slot = (int)(inf >> 20);
+  const int bits = (int)((inf >> 16) & 15), slot = (int)((inf >> 20) & 7);
   uint32_t e = S.u.lut[(inf & 0xffff) + (look >> (16 - bits))];
-  e = bits ? e : 0u;
-  if (e & 0x8000u) e = S.lut2[slot][e & (NSUB - 1)][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
-  if (e == 0) e = slow_entry(S, slot, look);
+  if ((e & 31) == 0) {
+    if (e) e = S.lut2[inf >> 23][(e >> 5) - 1][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
+    if ((e & 31) == 0) e = slow_entry(S, slot, look);
+  }
   return e;
 }
 
@@ -240,14 +251,19 @@ FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 
 
 // SYNC decode of a lane's range [st.pos, end_bit): counts the blocks started
 // in it and records their start events (the first NEV; row NEV is a dummy
-// the overflow writes go to).  With use_old (a later round) it stops at a
-// block start that matches an event of the lane's previous trajectory and
-// splices onto it: from an identical state the old trajectory is exact, so
-// its remaining count and exit state are reused.  The old-event cursor
-// advances one event per symbol (old events behind the decode position can
-// never match); lagging only delays a splice, never makes a wrong one.
-// Events are double-buffered: buffer cb holds the previous trajectory's,
-// cb ^ 1 receives the new one.
+// that absorbs every non-recording store).  With use_old (a later round) it
+// stops at a block start that matches an event of the lane's previous
+// trajectory and splices onto it: from an identical state the old trajectory
+// is exact, so its remaining count and exit state are reused.  The old-event
+// cursor advances one event per symbol (old events behind the decode
+// position can never match); lagging only delays a splice, never makes a
+// wrong one.  Events are double-buffered: buffer cb holds the previous
+// trajectory's, cb ^ 1 receives the new one.
+//
+// The loop body is straight-line except the refill, the second-level lookup
+// and the canonical fallback: with 64 lanes some lane starts or ends a block
+// on almost every step, so those updates are selects fed by loads issued at
+// the top of the step (next phase's table infos, next old event).
 FFCV_DEV DecState sync_range(JShared &S, const uint32_t *words, DecState st,
                              uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, DecState old_exit,
                              bool use_old, uint32_t &iters) {
@@ -256,52 +272,45 @@ FFCV_DEV DecState sync_range(JShared &S, const uint32_t *words, DecState st,
   uint32_t pos = st.pos;
   int z = st.z, ph = st.ph;
   const int bpm = S.bpm;
-  // table infos of this phase and (prefetched) of the next
   uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
-  int nph = ph + 1 == bpm ? 0 : ph + 1;
-  uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
   const int ob = cb, nbuf = cb ^ 1;
   const int onev = use_old ? nev : 0;
+  const uint32_t *evo = &S.ev[ob][0][lane];
+  uint32_t *evn = &S.ev[nbuf][0][lane];
   int j = 0;
-  uint32_t ocur = onev > 0 ? S.ev[ob][0][lane] : 0xFFFFFFFFu;
+  uint32_t ocur = onev > 0 ? evo[0] : 0xFFFFFFFFu;
   int n = 0;
-  bool spliced = false;
-  while (pos < end_bit) {
+  bool hit = false;
+  while (pos < end_bit && !hit) {
     iters++;
+    const int nph = ph + 1 == bpm ? 0 : ph + 1;
+    const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
+    const uint32_t onext = evo[min(j + 1, NEV) * JT];
     const bool isblk = z == 0;
     const uint32_t key = (pos << 4) | (uint32_t)ph;
-    const uint32_t onext = S.ev[ob][min(j + 1, NEV)][lane];
-    if (isblk) {
-      if (ocur == key) {
-        spliced = true;
-        break;
-      }
-      S.ev[nbuf][min(n, NEV)][lane] = key;
-      n++;
-    }
+    hit = isblk && ocur == key;
+    const bool rec = isblk && !hit;
+    evn[(rec ? min(n, NEV) : NEV) * JT] = key;
+    n += rec ? 1 : 0;
     const bool adv = ocur < key;
     j += adv ? 1 : 0;
     ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
     const uint32_t e = decode_entry(S, isblk ? dinf : ainf, br.acc);
-    const int nbits = (int)(e & 15) + 1 + ((int)(e >> 4) & 15);
+    const int nbits = hit ? 0 : (int)(e & 31);
     br.consume(nbits);
     pos += nbits;
-    z += (int)(e >> 8);
-    if (z >= 64) {
-      z = 0;
-      ph = nph;
-      dinf = ndinf;
-      ainf = nainf;
-      nph = ph + 1 == bpm ? 0 : ph + 1;
-      ndinf = S.dinf[nph];
-      nainf = S.ainf[nph];
-    }
+    z += hit ? 0 : (int)(e >> 9);
+    const bool bend = z >= 64;
+    z = bend ? 0 : z;
+    ph = bend ? nph : ph;
+    dinf = bend ? ndinf : dinf;
+    ainf = bend ? nainf : ainf;
   }
-  if (spliced) {  // at the previous trajectory's j-th block start
+  if (hit) {  // at the previous trajectory's j-th block start
     int m = n;
     if (n < NEV) {
       int keep = min(onev - j, NEV - n);
-      for (int q = 0; q < keep; q++) S.ev[nbuf][n + q][lane] = S.ev[ob][j + q][lane];
+      for (int q = 0; q < keep; q++) evn[(n + q) * JT] = evo[(j + q) * JT];
       m = n + keep;
     }
     nev = min(m, NEV);
@@ -322,9 +331,16 @@ FFCV_DEV DecState sync_range(JShared &S, const uint32_t *words, DecState st,
 // WRITE decode: DC differences of every block and the AC coefficients (in
 // zigzag order; the IDCT de-zigzags in registers) of the blocks inside the
 // window.  blk = index of the block in progress (z > 0) or of the next block
-// to start (z == 0).  The next phase's descriptor is prefetched one block
-// ahead, so a block start costs no LDS round trip; each symbol makes at most
-// one (predicated) 2-byte store.
+// to start (z == 0).  Straight-line like sync_range: the next block's
+// destination and window test are computed from the next phase's
+// descriptor (loaded at the top of the step) and selected at a block end.
+FFCV_DEV void locate_block(const int4 pd0, const int4 pd1, int64_t blk, int64_t nblocks, int mx, int my,
+                           uint32_t &boff, bool &inwin) {
+  // pd0 = {base block, blocks per MCU row, hs, mx_lo}, pd1 = {mx_hi, my_lo, my_hi, -}
+  inwin = blk < nblocks && mx >= pd0.w && mx <= pd1.x && my >= pd1.y && my <= pd1.z;
+  boff = ((uint32_t)pd0.x + (uint32_t)my * (uint32_t)pd0.y + (uint32_t)mx * (uint32_t)pd0.z) * 64u;
+}
+
 FFCV_DEV void write_range(JShared &S, const uint32_t *words, DecState st, uint32_t end_bit,
                           int64_t blk, int16_t *coef, int16_t *dcd, uint32_t &iters) {
   BitReader br;
@@ -334,69 +350,63 @@ FFCV_DEV void write_range(JShared &S, const uint32_t *words, DecState st, uint32
   const int bpm = S.bpm, mcux = S.mcux;
   const int64_t nblocks = S.nblocks;
   uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
-  int nph0 = ph + 1 == bpm ? 0 : ph + 1;
-  uint32_t ndinf = S.dinf[nph0], nainf = S.ainf[nph0];
   int m = (int)(blk / bpm);
   int my = m / mcux, mx = m - my * mcux;
-  int16_t *bptr = coef;
-  bool inwin = false;
-  int4 pd0 = S.pdesc[ph][0], pd1 = S.pdesc[ph][1];
-  auto locate = [&]() {
-    // pd0 = {base block, blocks per MCU row, hs, mx_lo}, pd1 = {mx_hi, my_lo, my_hi, -}
-    inwin = blk < nblocks && mx >= pd0.w && mx <= pd1.x && my >= pd1.y && my <= pd1.z;
-    bptr = coef + ((uint64_t)(uint32_t)pd0.x + (uint64_t)my * (uint32_t)pd0.y + (uint64_t)mx * pd0.z) * 64;
-    const int nph = ph + 1 == bpm ? 0 : ph + 1;
-    pd0 = S.pdesc[nph][0];
-    pd1 = S.pdesc[nph][1];
-  };
-  if (z > 0) locate();
-  while (pos < end_bit) {
+  uint32_t boff;
+  bool inwin;
+  locate_block(S.pdesc[ph][0], S.pdesc[ph][1], blk, nblocks, mx, my, boff, inwin);
+  while (pos < end_bit && !(z == 0 && blk >= nblocks)) {
     iters++;
+    const int nph = ph + 1 == bpm ? 0 : ph + 1;
+    const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
+    const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
     const bool isblk = z == 0;
-    if (isblk) {
-      if (blk >= nblocks) break;
-      locate();
-    }
     const uint32_t e = decode_entry(S, isblk ? dinf : ainf, br.acc);
-    const int len = (int)(e & 15) + 1, size = (int)(e >> 4) & 15, zinc = (int)(e >> 8);
-    const int raw = (int)((br.acc << len) >> 1 >> (63 - size));
+    const int nbits = (int)(e & 31), size = (int)(e >> 5) & 15, zinc = (int)(e >> 9);
+    const int raw = (int)((br.acc << (nbits - size)) >> 1 >> (63 - size));
     const int v = size ? huff_extend(raw, size) : 0;
-    br.consume(len + size);
-    pos += len + size;
-    int16_t *dst = isblk ? dcd + blk : bptr + min(z + zinc - 1, 63);
+    br.consume(nbits);
+    pos += nbits;
+    int16_t *dst = isblk ? dcd + blk : coef + boff + min(z + zinc - 1, 63);
     if (isblk || (size && inwin)) *dst = (int16_t)v;
     z += zinc;
-    if (z >= 64) {
-      z = 0;
-      blk++;
-      ph++;
-      if (ph == bpm) {
-        ph = 0;
-        if (++mx == mcux) {
-          mx = 0;
-          my++;
-        }
-      }
-      dinf = ndinf;
-      ainf = nainf;
-      const int np = ph + 1 == bpm ? 0 : ph + 1;
-      ndinf = S.dinf[np];
-      nainf = S.ainf[np];
-    }
+    const bool bend = z >= 64;
+    // the next block: (blk + 1, nph, mx', my')
+    const bool wrap = nph == 0;
+    const int nmx = wrap ? (mx + 1 == mcux ? 0 : mx + 1) : mx;
+    const int nmy = wrap && mx + 1 == mcux ? my + 1 : my;
+    uint32_t nboff;
+    bool ninwin;
+    locate_block(npd0, npd1, blk + 1, nblocks, nmx, nmy, nboff, ninwin);
+    z = bend ? 0 : z;
+    blk += bend ? 1 : 0;
+    ph = bend ? nph : ph;
+    mx = bend ? nmx : mx;
+    my = bend ? nmy : my;
+    dinf = bend ? ndinf : dinf;
+    ainf = bend ? nainf : ainf;
+    boff = bend ? nboff : boff;
+    inwin = bend ? ninwin : inwin;
   }
 }
 
-// Exclusive prefix sum over the wave.
+// Cross-lane helpers on DPP (no LDS round trip, unlike __shfl's
+// ds_bpermute).  All lanes of the wave must be active.
+//   wave_exscan: exclusive prefix sum (row_shr 1/2/4/8, row_bcast 15/31)
+//   lane_prev / lane_next: value of lane t-1 / t+1 (0 past the ends)
 FFCV_DEV uint32_t wave_exscan(uint32_t v) {
-  const int lane = threadIdx.x;
-  uint32_t x = v;
-#pragma unroll
-  for (int off = 1; off < JT; off <<= 1) {
-    uint32_t y = __shfl_up(x, off);
-    x += lane >= off ? y : 0u;
-  }
-  return x - v;
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return (uint32_t)x - v;
 }
+FFCV_DEV uint32_t lane_prev(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false); }
+FFCV_DEV uint32_t lane_next(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false); }
+FFCV_DEV uint32_t lane_read(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
 FFCV_DEV int32_t wave_exscan_i(int32_t v) { return (int32_t)wave_exscan((uint32_t)v); }
 
 
@@ -405,78 +415,68 @@ FFCV_DEV uint8_t idct_rl(int x) {
   int v = x & 1023;
   return (uint8_t)(v < 128 ? v + 128 : (v < 512 ? 255 : (v < 896 ? 0 : v - 896)));
 }
-FFCV_DEV int fmul8(int v, int c) { return (int)(((int64_t)v * c) >> 8); }
+// jidctfst.c MULTIPLY: DESCALE(var * const, CONST_BITS = 8) with a JLONG
+// (64-bit) product.  The 32-bit form is identical whenever the product fits,
+// which holds for every dequantised input below 2^14 in magnitude (all valid
+// 8-bit baseline data); WIDE keeps the exact 64-bit form for the rest.
+template <bool WIDE>
+FFCV_DEV int fmul8(int v, int c) {
+  return WIDE ? (int)(((int64_t)v * c) >> 8) : (v * c) >> 8;
+}
 
-// jidctfst.c jpeg_idct_ifast on one block.
-FFCV_DEV void idct_ifast_block(const int16_t *in, const int16_t *q, uint8_t *out, int stride) {
-  int ws[64];
+// jidctfst.c jpeg_idct_ifast on one dequantised block d (natural order),
+// straight-line: the reference's all-zero-AC shortcuts produce the same
+// values, so they are not taken (they would only diverge the wave).
+template <bool WIDE>
+FFCV_DEV void idct_ifast_block(int d[64], uint8_t *out, int stride) {
 #pragma unroll
   for (int c = 0; c < 8; c++) {
-    int i0 = in[c], i1 = in[8 + c], i2 = in[16 + c], i3 = in[24 + c], i4 = in[32 + c], i5 = in[40 + c],
-        i6 = in[48 + c], i7 = in[56 + c];
-    if ((i1 | i2 | i3 | i4 | i5 | i6 | i7) == 0) {
-      int dc = i0 * q[c];
-#pragma unroll
-      for (int r = 0; r < 8; r++) ws[8 * r + c] = dc;
-      continue;
-    }
-    int tmp0 = i0 * q[c], tmp1 = i2 * q[16 + c], tmp2 = i4 * q[32 + c], tmp3 = i6 * q[48 + c];
+    int tmp0 = d[c], tmp1 = d[16 + c], tmp2 = d[32 + c], tmp3 = d[48 + c];
     int tmp10 = tmp0 + tmp2, tmp11 = tmp0 - tmp2;
-    int tmp13 = tmp1 + tmp3, tmp12 = fmul8(tmp1 - tmp3, 362) - tmp13;
+    int tmp13 = tmp1 + tmp3, tmp12 = fmul8<WIDE>(tmp1 - tmp3, 362) - tmp13;
     tmp0 = tmp10 + tmp13;
     tmp3 = tmp10 - tmp13;
     tmp1 = tmp11 + tmp12;
     tmp2 = tmp11 - tmp12;
-    int tmp4 = i1 * q[8 + c], tmp5 = i3 * q[24 + c], tmp6 = i5 * q[40 + c], tmp7 = i7 * q[56 + c];
+    int tmp4 = d[8 + c], tmp5 = d[24 + c], tmp6 = d[40 + c], tmp7 = d[56 + c];
     int z13 = tmp6 + tmp5, z10 = tmp6 - tmp5, z11 = tmp4 + tmp7, z12 = tmp4 - tmp7;
     tmp7 = z11 + z13;
-    tmp11 = fmul8(z11 - z13, 362);
-    int z5 = fmul8(z10 + z12, 473);
-    tmp10 = fmul8(z12, 277) - z5;
-    tmp12 = fmul8(z10, -669) + z5;
+    tmp11 = fmul8<WIDE>(z11 - z13, 362);
+    int z5 = fmul8<WIDE>(z10 + z12, 473);
+    tmp10 = fmul8<WIDE>(z12, 277) - z5;
+    tmp12 = fmul8<WIDE>(z10, -669) + z5;
     tmp6 = tmp12 - tmp7;
     tmp5 = tmp11 - tmp6;
     tmp4 = tmp10 + tmp5;
-    ws[c] = tmp0 + tmp7;
-    ws[56 + c] = tmp0 - tmp7;
-    ws[8 + c] = tmp1 + tmp6;
-    ws[48 + c] = tmp1 - tmp6;
-    ws[16 + c] = tmp2 + tmp5;
-    ws[40 + c] = tmp2 - tmp5;
-    ws[32 + c] = tmp3 + tmp4;
-    ws[24 + c] = tmp3 - tmp4;
+    d[c] = tmp0 + tmp7;
+    d[56 + c] = tmp0 - tmp7;
+    d[8 + c] = tmp1 + tmp6;
+    d[48 + c] = tmp1 - tmp6;
+    d[16 + c] = tmp2 + tmp5;
+    d[40 + c] = tmp2 - tmp5;
+    d[32 + c] = tmp3 + tmp4;
+    d[24 + c] = tmp3 - tmp4;
   }
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    const int *w = ws + 8 * r;
-    uint8_t o[8];
-    if ((w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) == 0) {
-      uint8_t dc = idct_rl(w[0] >> 5);
-#pragma unroll
-      for (int q2 = 0; q2 < 8; q2++) o[q2] = dc;
-    } else {
-      int tmp10 = w[0] + w[4], tmp11 = w[0] - w[4];
-      int tmp13 = w[2] + w[6], tmp12 = fmul8(w[2] - w[6], 362) - tmp13;
-      int tmp0 = tmp10 + tmp13, tmp3 = tmp10 - tmp13, tmp1 = tmp11 + tmp12, tmp2 = tmp11 - tmp12;
-      int z13 = w[5] + w[3], z10 = w[5] - w[3], z11 = w[1] + w[7], z12 = w[1] - w[7];
-      int tmp7 = z11 + z13;
-      tmp11 = fmul8(z11 - z13, 362);
-      int z5 = fmul8(z10 + z12, 473);
-      tmp10 = fmul8(z12, 277) - z5;
-      tmp12 = fmul8(z10, -669) + z5;
-      int tmp6 = tmp12 - tmp7, tmp5 = tmp11 - tmp6, tmp4 = tmp10 + tmp5;
-      o[0] = idct_rl((tmp0 + tmp7) >> 5);
-      o[7] = idct_rl((tmp0 - tmp7) >> 5);
-      o[1] = idct_rl((tmp1 + tmp6) >> 5);
-      o[6] = idct_rl((tmp1 - tmp6) >> 5);
-      o[2] = idct_rl((tmp2 + tmp5) >> 5);
-      o[5] = idct_rl((tmp2 - tmp5) >> 5);
-      o[4] = idct_rl((tmp3 + tmp4) >> 5);
-      o[3] = idct_rl((tmp3 - tmp4) >> 5);
-    }
+    const int *w = d + 8 * r;
+    int tmp10 = w[0] + w[4], tmp11 = w[0] - w[4];
+    int tmp13 = w[2] + w[6], tmp12 = fmul8<WIDE>(w[2] - w[6], 362) - tmp13;
+    int tmp0 = tmp10 + tmp13, tmp3 = tmp10 - tmp13, tmp1 = tmp11 + tmp12, tmp2 = tmp11 - tmp12;
+    int z13 = w[5] + w[3], z10 = w[5] - w[3], z11 = w[1] + w[7], z12 = w[1] - w[7];
+    int tmp7 = z11 + z13;
+    tmp11 = fmul8<WIDE>(z11 - z13, 362);
+    int z5 = fmul8<WIDE>(z10 + z12, 473);
+    tmp10 = fmul8<WIDE>(z12, 277) - z5;
+    tmp12 = fmul8<WIDE>(z10, -669) + z5;
+    int tmp6 = tmp12 - tmp7, tmp5 = tmp11 - tmp6, tmp4 = tmp10 + tmp5;
+    uint32_t o0 = idct_rl((tmp0 + tmp7) >> 5), o7 = idct_rl((tmp0 - tmp7) >> 5);
+    uint32_t o1 = idct_rl((tmp1 + tmp6) >> 5), o6 = idct_rl((tmp1 - tmp6) >> 5);
+    uint32_t o2 = idct_rl((tmp2 + tmp5) >> 5), o5 = idct_rl((tmp2 - tmp5) >> 5);
+    uint32_t o4 = idct_rl((tmp3 + tmp4) >> 5), o3 = idct_rl((tmp3 - tmp4) >> 5);
     uint2 v;
-    v.x = o[0] | (o[1] << 8) | (o[2] << 16) | ((uint32_t)o[3] << 24);
-    v.y = o[4] | (o[5] << 8) | (o[6] << 16) | ((uint32_t)o[7] << 24);
+    v.x = o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
+    v.y = o4 | (o5 << 8) | (o6 << 16) | (o7 << 24);
     *(uint2 *)(out + (uint64_t)r * stride) = v;
   }
 }
@@ -655,12 +655,14 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
         }
       }
       // first-level LUT space from the pool, in slot order (AC slots first)
-      uint32_t used = 0;
+      uint32_t used = 0, nset = 0;
       for (int q = 0; q < S.nslots; q++) {
         uint32_t bits = S.slot_tab[q] >= 4 ? FB_AC : FB_DC;
-        if (used + (1u << bits) > LUT_POOL) bits = 0;  // canonical decode only
-        S.sinfo[q] = (bits ? used : 0u) | (bits << 16) | ((uint32_t)q << 20);
+        if (used + (1u << bits) > LUT_POOL - 1 || nset == NLUTSLOT) bits = 0;  // canonical decode only
+        S.sinfo[q] = (bits ? used : (uint32_t)(LUT_POOL - 1)) | (bits << 16) | ((uint32_t)q << 20) |
+                     ((bits ? nset : 0u) << 23);
         used += bits ? (1u << bits) : 0u;
+        nset += bits ? 1u : 0u;
       }
       for (int b = 0; b < nb; b++) {
         S.dinf[b] = S.sinfo[slot_of(S.dcpack, b)];
@@ -847,13 +849,19 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
       S.lim[t][l] = code << (16 - l);
       code <<= 1;
     }
-    for (int i = 0; i < kk; i++) {
-      int v = HB(d + 16 + i);
-      if (tab < 4 && v > 15) bad = true;  // DC sizes are 0..15
-      S.vals[t][i] = (uint8_t)v;
-    }
+    S.nvals[t] = kk;
     if (bad) S.status = FFCV_SAMPLE_BAD_MARKER;
     S.nsub[t] = 0;
+  }
+  __syncthreads();
+  for (int s2 = 0; s2 < S.nslots; s2++) {
+    const int tab = S.slot_tab[s2];
+    const uint32_t d = S.dht_off[tab];
+    for (int i = t; i < S.nvals[s2]; i += JT) {
+      int v = HB(d + 16 + i);
+      if (tab < 4 && v > 15) S.status = FFCV_SAMPLE_BAD_MARKER;  // DC sizes are 0..15
+      S.vals[s2][i] = (uint8_t)v;
+    }
   }
   for (int i = t; i < S.ncomp * 64; i += JT) {
     int c = i >> 6, zz = i & 63;
@@ -861,7 +869,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     uint32_t q = S.dqt_off[tq];
     int qv = S.dqt_prec[tq] ? ((HB(q + 2 * zz) << 8) | HB(q + 2 * zz + 1)) : HB(q + zz);
     int n = c_natural[zz];
-    S.qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
+    info->qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
   }
   __syncthreads();  // header bytes are dead from here (the LUT pool reuses them)
   if (S.status != FFCV_SAMPLE_OK) {
@@ -869,15 +877,20 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     return;
   }
   const int nslots = S.nslots;
+  if (t == 0) S.u.lut[LUT_POOL - 1] = 0;  // the zero word of LUT-less slots
   for (int s = 0; s < nslots; s++) {
     const uint32_t inf = S.sinfo[s];
     const int bits = (int)((inf >> 16) & 15);
     if (!bits) continue;
     const bool ac = (S.acmask >> s) & 1;
+    uint32_t L[FB_AC + 1];
+#pragma unroll
+    for (int l = 1; l <= FB_AC; l++) L[l] = S.lim[s][l];
     for (int v = t; v < (1 << bits); v += JT) {
       const uint32_t look = (uint32_t)v << (16 - bits);
       int len = 1;
-      for (int l = 1; l < bits; l++) len += look >= S.lim[s][l];
+#pragma unroll
+      for (int l = 1; l < FB_AC; l++) len += (l < bits && look >= L[l]) ? 1 : 0;
       uint32_t e = 0;
       if (look < S.lim[s][len]) {
         int sym = S.vals[s][(S.valoff[s][len] + (int)(look >> (16 - len))) & 0xff];
@@ -886,7 +899,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
         int n = atomicAdd(&S.nsub[s], 1);
         if (n < NSUB) {
           S.sub_prefix[s][n] = (uint16_t)v;
-          e = 0x8000u | (uint32_t)n;
+          e = (uint32_t)(n + 1) << 5;
         }
       }
       S.u.lut[(inf & 0xffff) + v] = (uint16_t)e;
@@ -900,7 +913,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     const uint32_t look = ((uint32_t)S.sub_prefix[s][n] << (16 - bits)) | ((uint32_t)x << (16 - bits - SUBB));
     int len = 1;
     for (int l = 1; l < 16; l++) len += look >= S.lim[s][l];
-    S.lut2[s][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(S, s, look) : (uint16_t)0;
+    S.lut2[S.sinfo[s] >> 23][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(S, s, look) : (uint16_t)0;
   }
   // the coefficient slot is all zeros here: the IDCT kernel zeroes every
   // block it consumes (and ffcv_jpeg_create zeroed the slot)
@@ -922,57 +935,90 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     const uint32_t *aw = (const uint32_t *)(sb - mis);
     const uint32_t ndw = (seglen + mis + 3) / 4;
     uint32_t carry = 0;  // byte before this step's first byte (0: none / not 0xFF)
-    // 4-deep prefetch ring: step i works on r0 while steps i+1..i+3 load
+    // Kept bytes are staged in LDS and flushed to HBM as aligned dwords every
+    // DS_FLUSH steps: a byte store per kept byte would make every prefetch
+    // wait behind the stores (gfx9 counts loads and stores in one vmcnt).
+    uint32_t fbase = 0;  // stream offset of stage[0] (a multiple of 4)
+    auto flush = [&](uint32_t upto) {  // write stage bytes [fbase, upto), upto % 4 == 0
+      __syncthreads();
+      const uint32_t nd = (upto - fbase) / 4;
+      for (uint32_t q = t; q < nd; q += JT) ((uint32_t *)gds)[fbase / 4 + q] = ((const uint32_t *)S.stage)[q];
+      __syncthreads();
+    };
+    // DS_DEPTH-deep prefetch ring, unrolled so every ring register is consumed in
+    // place (a rotating copy would make the compiler wait for all loads)
     auto ld = [&](uint32_t d) -> uint32_t { return d < ndw ? __builtin_nontemporal_load(aw + d) : 0u; };
-    uint32_t r0 = ld(t), r1 = ld(JT + t), r2 = ld(2 * JT + t), r3 = ld(3 * JT + t);
-    for (uint32_t base = 0; base < ndw; base += JT) {
-      const uint32_t di = base + t;
-      const uint32_t w = r0;
-      r0 = r1;
-      r1 = r2;
-      r2 = r3;
-      r3 = ld(base + 4 * JT + t);
-      const uint32_t wprev = __shfl_up(w, 1);
-      const uint32_t wnext = __shfl_down(w, 1);
-      const uint32_t nfirst = __shfl(r0, 0);  // next step's first dword
-      const uint32_t prevb = t == 0 ? carry : (wprev >> 24);
-      const uint32_t next0 = (t == JT - 1 ? nfirst : wnext) & 0xff;
-      int first_mk = 4;  // first marker byte index in this dword
-      uint32_t keepm = 0;
+    uint32_t r[DS_DEPTH];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int rel = (int)(4 * di + j) - (int)mis;
-        const bool valid = rel >= 0 && rel < (int)seglen;
-        const uint32_t b = (w >> (8 * j)) & 0xff;
-        const uint32_t pb = j == 0 ? prevb : (w >> (8 * j - 8)) & 0xff;
-        uint32_t nx = j == 3 ? next0 : (w >> (8 * j + 8)) & 0xff;
-        nx = rel + 1 < (int)seglen ? nx : 0xD9u;  // end of data acts as a marker
-        const bool removed = rel > 0 && b == 0 && pb == 0xFF;
-        const bool marker = valid && b == 0xFF && nx != 0;
-        if (marker && first_mk == 4) first_mk = j;
-        if (valid && !removed) keepm |= 1u << j;
-      }
-      // the first marker of the step ends the segment
-      const uint64_t mk = __ballot(first_mk < 4);
-      bool stop = false;
-      if (mk) {
-        const int ml = __ffsll((unsigned long long)mk) - 1;
-        const int mj = __shfl(first_mk, ml);
-        if (t > ml) keepm = 0;
-        if (t == ml) keepm &= (1u << mj) - 1;
-        stop = true;
-      }
-      const uint32_t cnt = __popc(keepm);
-      uint32_t off = dlen + wave_exscan(cnt);
+    for (int u = 0; u < DS_DEPTH; u++) r[u] = ld(u * JT + t);
+    int step = 0;
+    bool done = false;
+    for (uint32_t base4 = 0; !done; base4 += DS_DEPTH * JT) {
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (keepm & (1u << j)) gds[off++] = (uint8_t)(w >> (8 * j));
-      dlen = __shfl(off, JT - 1);
-      carry = __shfl(w, JT - 1) >> 24;
-      if (stop) break;
+      for (int u = 0; u < DS_DEPTH; u++) {
+        const uint32_t base = base4 + u * JT;
+        if (done || base >= ndw) {
+          done = true;
+          continue;
+        }
+        const uint32_t di = base + t;
+        const uint32_t w = r[u];
+        r[u] = ld(base + DS_DEPTH * JT + t);
+        const uint32_t wprev = lane_prev(w);
+        const uint32_t wnext = lane_next(w);
+        const uint32_t nfirst = lane_read(r[(u + 1) % DS_DEPTH], 0);  // next step's first dword
+        const uint32_t prevb = t == 0 ? carry : (wprev >> 24);
+        const uint32_t next0 = (t == JT - 1 ? nfirst : wnext) & 0xff;
+        // SWAR over the 4 bytes (byte j = stream byte 4*di + j - mis):
+        // zm(x) has 0x80 in every byte of x that is zero
+        auto zm = [](uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
+        auto bits4 = [](uint32_t m80) { return (((m80 >> 7) & 0x01010101u) * 0x01020408u) >> 24; };
+        const uint32_t pw = (w << 8) | prevb;          // previous byte of each byte
+        const uint32_t nw = (w >> 8) | (next0 << 24);  // next byte of each byte
+        const int rel0 = (int)(4 * di) - (int)mis;     // stream index of byte 0
+        const int lo = max(0, -rel0), hi = min(4, (int)seglen - rel0);  // valid bytes [lo, hi)
+        const uint32_t valid4 = hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+        const uint32_t ff = zm(~w);
+        // a 0x00 after 0xFF is stuffing, except the segment's first byte
+        const uint32_t head = rel0 <= 0 ? (2u << min(3, -rel0)) - 1u : 0u;  // bytes with rel <= 0
+        const uint32_t removed4 = bits4(zm(w) & zm(~pw)) & ~head;
+        // a marker is 0xFF followed by a non-zero byte; end of data acts as one
+        const uint32_t lastm = (hi >= 1 && hi <= 4 && rel0 + hi == (int)seglen) ? 1u << (hi - 1) : 0u;
+        const uint32_t mark4 = (bits4(ff & ~zm(nw)) | (bits4(ff) & lastm)) & valid4;
+        const int first_mk = mark4 ? __builtin_ctz(mark4) : 4;
+        uint32_t keepm = valid4 & ~removed4 & ((1u << first_mk) - 1u);
+        // the first marker of the step ends the segment
+        const uint64_t mk = __ballot(first_mk < 4);
+        if (mk) {
+          const int ml = __ffsll((unsigned long long)mk) - 1;
+          if (t > ml) keepm = 0;
+          done = true;
+        }
+        const uint32_t cnt = __popc(keepm);
+        uint32_t off = dlen + wave_exscan(cnt) - fbase;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {  // branch-free: dropped bytes go to a dummy byte
+          const bool kj = (keepm >> j) & 1;
+          S.stage[kj ? off + __popc(keepm & ((1u << j) - 1u)) : STAGE_DUMMY] = (uint8_t)(w >> (8 * j));
+        }
+        off += cnt;
+        dlen = lane_read(off, JT - 1) + fbase;
+        carry = lane_read(w, JT - 1) >> 24;
+      }
+      if (!done && (step += DS_DEPTH) == DS_FLUSH) {  // flush whole dwords, keep the 0..3-byte tail
+        step = 0;
+        const uint32_t upto = dlen & ~3u;
+        flush(upto);
+        if (t < (int)(dlen - upto)) S.stage[t] = S.stage[upto - fbase + t];
+        fbase = upto;
+        __syncthreads();
+      }
     }
+    // tail + zero padding (libjpeg fills zeros after a marker)
+    __syncthreads();
+    for (uint32_t i = dlen - fbase + t; i < dlen - fbase + STREAM_PAD + 4; i += JT) S.stage[i] = 0;
+    flush((dlen + STREAM_PAD + 3) & ~3u);
   }
-  if (t < STREAM_PAD) gds[dlen + t] = 0;  // zero fill, as libjpeg past a marker
   __threadfence_block();
   __syncthreads();
   const uint32_t *words = (const uint32_t *)gds;
@@ -998,9 +1044,9 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
   int rounds = 0;
   for (;;) {
     DecState ng;
-    ng.pos = __shfl_up(e.pos, 1);
-    ng.z = __shfl_up(e.z, 1);
-    ng.ph = __shfl_up(e.ph, 1);
+    ng.pos = lane_prev(e.pos);
+    ng.z = (int)lane_prev((uint32_t)e.z);
+    ng.ph = (int)lane_prev((uint32_t)e.ph);
     const bool changed = active && t > 0 && (ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph);
     if (!__any(changed)) break;
     rounds++;
@@ -1120,7 +1166,6 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
   // ------------------------------------------------------------- P7 ----
   // geometry + window + multipliers for jpeg_idct_kernel and K2
   STAMP(7);
-  for (int i = t; i < 3 * 64; i += JT) info->qmul[i >> 6][i & 63] = (i >> 6) < S.ncomp ? S.qmul[i >> 6][i & 63] : 0;
   if (t == 0) {
     info->status = FFCV_SAMPLE_OK;
     info->W = S.W;
@@ -1176,16 +1221,27 @@ __global__ void __launch_bounds__(IDCT_T) jpeg_idct_kernel(JpegArgs a) {
   const int wbw = I->wbw[c];
   const int by = I->wy0[c] + i / wbw, bx = I->wx0[c] + i % wbw;
   int16_t *cp = a.coef + a.coef_slot * k + (I->coff[c] + (uint64_t)by * I->bw[c] + bx) * 64;
-  int16_t zz[64], blk[64];
+  int16_t zz[64], q[64];
+  int d[64];
 #pragma unroll
   for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
 #pragma unroll
-  for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
+  for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(q + p8 * 8) = ((const uint4 *)I->qmul[c])[p8];
 #pragma unroll
-  for (int n = 0; n < 64; n++) blk[n] = zz[kZigzagOfNatural[n]];
+  for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
+  // de-zigzag + jidctfst.c DEQUANTIZE (int16 x int16 -> int)
+  int mag = 0;
+#pragma unroll
+  for (int n = 0; n < 64; n++) {
+    d[n] = (int)zz[kZigzagOfNatural[n]] * (int)q[n];
+    mag |= d[n] < 0 ? -d[n] : d[n];
+  }
   const int stride = I->stride[c];
-  idct_ifast_block(blk, I->qmul[c], a.planes + a.plane_slot * k + I->poff[c] + (uint64_t)by * 8 * stride + bx * 8,
-                   stride);
+  uint8_t *out = a.planes + a.plane_slot * k + I->poff[c] + (uint64_t)by * 8 * stride + bx * 8;
+  if (mag < (1 << 14))
+    idct_ifast_block<false>(d, out, stride);
+  else
+    idct_ifast_block<true>(d, out, stride);
 }
 
 // ======================================================================= //

@@ -64,6 +64,7 @@ typedef struct {
 static int heur = 0;
 static long steps;
 
+static uint32_t rec_from = 0;  // events / counts only at positions >= rec_from
 static St run(St s, uint32_t end, Traj *t, const Traj *old, int spec) {
   int z = s.z, ph = s.ph;
   uint32_t pos = s.pos;
@@ -85,8 +86,10 @@ static St run(St s, uint32_t end, Traj *t, const Traj *old, int spec) {
           return nt.exit;
         }
       }
-      if (n < MAXEV) nt.ev[n++] = key;
-      started++;
+      if (pos >= rec_from) {
+        if (n < MAXEV) nt.ev[n++] = key;
+        started++;
+      }
     }
     steps++;
     int len, bad;
@@ -282,10 +285,15 @@ int main(int argc, char **argv) {
   Traj *T = calloc(lanes, sizeof(Traj));
   St *g = calloc(lanes, sizeof(St));
   long maxs = 0, tot = 0, wave_iters = 0, wmax[64] = {0};
+  int warm = argc > 4 ? atoi(argv[4]) : 0;
   for (int t = 0; t < lanes; t++) {
     g[t].pos = t * cb;
     steps = 0;
-    run(g[t], t == lanes - 1 ? tbits : (t + 1) * cb, &T[t], NULL, t > 0);
+    St st0 = g[t];
+    st0.pos = t * cb > (uint32_t)warm ? t * cb - warm : 0;
+    rec_from = t * cb;
+    run(t == 0 ? g[t] : st0, t == lanes - 1 ? tbits : (t + 1) * cb, &T[t], NULL, t > 0);
+    rec_from = 0;
     if (steps > maxs) maxs = steps;
     if (steps > wmax[t / 64]) wmax[t / 64] = steps;
     tot += steps;

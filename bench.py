@@ -134,7 +134,7 @@ def main():
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)
-    ap.add_argument('--inflight', type=int, default=2,
+    ap.add_argument('--inflight', type=int, default=3,
                     help='batches in flight on separate HIP streams (Loader batches_ahead analogue)')
     args = ap.parse_args()
 

@@ -231,7 +231,14 @@ struct AreaTaps {
   int lo, hi;       // inclusive source range
   int left, right;  // partial-tap indices (or -1)
   float wl, wf, wr;
-  FFCV_DEV float w(int s) const { return s == left ? wl : (s == right ? wr : wf); }
+  // s == left ? wl : (s == right ? wr : wf), as register selects (a plain
+  // ternary on members becomes a scratch-array lookup)
+  FFCV_DEV float w(int s) const {
+    uint32_t r = __float_as_uint(wf);
+    r = s == right ? __float_as_uint(wr) : r;
+    r = s == left ? __float_as_uint(wl) : r;
+    return __uint_as_float(r);
+  }
 };
 FFCV_DEV AreaTaps area_taps(int ssize, double scale, int d) {
   AreaTaps t;
@@ -280,12 +287,87 @@ FFCV_DEV void linear_coef(double scale, double inv, int ssize, int d, int *s_out
   *c1 = (int16_t)sat_s16i(__float2int_rn(f * 2048.f));
 }
 
+// Linear taps of one destination index (linear_coef, precomputable).
+struct LinTap {
+  int s;
+  int c0, c1;
+  int border;
+};
+FFCV_DEV LinTap lin_tap(double scale, double inv, int ssize, int d) {
+  LinTap t;
+  int16_t c0, c1;
+  bool b;
+  linear_coef(scale, inv, ssize, d, &t.s, &c0, &c1, &b);
+  t.c0 = c0;
+  t.c1 = c1;
+  t.border = b;
+  return t;
+}
+
 // Source accessor: pixel (y, x) channel c of the ROI.
 struct RoiSrc {
   const uint8_t *p;
   uint64_t step;  // bytes per row
   FFCV_DEV int at(int y, int x, int c) const { return p[(uint64_t)y * step + (uint64_t)x * 3 + c]; }
 };
+
+// INTER_AREA general path for one output pixel from its column/row taps.
+template <class Src>
+FFCV_DEV void resize_area(const Src &S, const AreaTaps &tx, const AreaTaps &ty, int out[3]) {
+  float sum0 = 0.f, sum1 = 0.f, sum2 = 0.f;
+  for (int sy = ty.lo; sy <= ty.hi; sy++) {
+    float buf0 = 0.f, buf1 = 0.f, buf2 = 0.f;
+    for (int sx = tx.lo; sx <= tx.hi; sx++) {
+      const float a = tx.w(sx);
+      buf0 = buf0 + (float)S.at(sy, sx, 0) * a;
+      buf1 = buf1 + (float)S.at(sy, sx, 1) * a;
+      buf2 = buf2 + (float)S.at(sy, sx, 2) * a;
+    }
+    const float beta = ty.w(sy);
+    if (sy == ty.lo) {
+      sum0 = beta * buf0;
+      sum1 = beta * buf1;
+      sum2 = beta * buf2;
+    } else {
+      sum0 = sum0 + beta * buf0;
+      sum1 = sum1 + beta * buf1;
+      sum2 = sum2 + beta * buf2;
+    }
+  }
+  out[0] = sat_u8i(__float2int_rn(sum0));
+  out[1] = sat_u8i(__float2int_rn(sum1));
+  out[2] = sat_u8i(__float2int_rn(sum2));
+}
+
+// Area-mode linear (Q11) path for one output pixel; dx is the destination
+// column (the SSE2-body / scalar-tail split depends on it).
+template <class Src>
+FFCV_DEV void resize_linear(const ResizePlan &P, const Src &S, int dx, const LinTap &lx, const LinTap &ly,
+                            int out[3]) {
+  const int sx = lx.s, sy = ly.s;
+  const int r0 = sy < 0 ? 0 : (sy >= P.sh ? P.sh - 1 : sy);
+  const int r1 = sy + 1 < 0 ? 0 : (sy + 1 >= P.sh ? P.sh - 1 : sy + 1);
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    int h0, h1;
+    if (lx.border) {
+      h0 = S.at(r0, sx, c) * 2048;
+      h1 = S.at(r1, sx, c) * 2048;
+    } else {
+      h0 = S.at(r0, sx, c) * lx.c0 + S.at(r0, sx + 1, c) * lx.c1;
+      h1 = S.at(r1, sx, c) * lx.c0 + S.at(r1, sx + 1, c) * lx.c1;
+    }
+    const int e = dx * 3 + c;
+    if (e < P.vec_end) {
+      int s0 = sat_s16i(h0 >> 4), s1 = sat_s16i(h1 >> 4);
+      int m0 = (s0 * ly.c0) >> 16, m1 = (s1 * ly.c1) >> 16;
+      int t = sat_s16i(m0 + m1);
+      out[c] = sat_u8i((t + 2) >> 2);
+    } else {
+      out[c] = sat_u8i((h0 * ly.c0 + h1 * ly.c1 + (1 << 21)) >> 22);
+    }
+  }
+}
 
 // Compute the 3 channels of output pixel (dy, dx).
 template <class Src>
@@ -306,58 +388,10 @@ FFCV_DEV void resize_pixel(const ResizePlan &P, const Src &S, int dy, int dx, in
     return;
   }
   if (P.kind == 2) {
-    AreaTaps tx = area_taps(P.sw, P.scale_x, dx);
-    AreaTaps ty = area_taps(P.sh, P.scale_y, dy);
-    float sum[3] = {0.f, 0.f, 0.f};
-    for (int sy = ty.lo; sy <= ty.hi; sy++) {
-      float buf[3] = {0.f, 0.f, 0.f};
-      for (int sx = tx.lo; sx <= tx.hi; sx++) {
-        float a = tx.w(sx);
-        buf[0] = buf[0] + (float)S.at(sy, sx, 0) * a;
-        buf[1] = buf[1] + (float)S.at(sy, sx, 1) * a;
-        buf[2] = buf[2] + (float)S.at(sy, sx, 2) * a;
-      }
-      float beta = ty.w(sy);
-      if (sy == ty.lo) {
-        sum[0] = beta * buf[0];
-        sum[1] = beta * buf[1];
-        sum[2] = beta * buf[2];
-      } else {
-        sum[0] = sum[0] + beta * buf[0];
-        sum[1] = sum[1] + beta * buf[1];
-        sum[2] = sum[2] + beta * buf[2];
-      }
-    }
-    for (int c = 0; c < 3; c++) out[c] = sat_u8i(__float2int_rn(sum[c]));
+    resize_area(S, area_taps(P.sw, P.scale_x, dx), area_taps(P.sh, P.scale_y, dy), out);
     return;
   }
-  // kind 3: linear Q11
-  int sx, sy;
-  int16_t a0, a1, b0, b1;
-  bool bx, by_unused;
-  linear_coef(P.scale_x, P.inv_x, P.sw, dx, &sx, &a0, &a1, &bx);
-  linear_coef(P.scale_y, P.inv_y, P.sh, dy, &sy, &b0, &b1, &by_unused);
-  int r0 = sy < 0 ? 0 : (sy >= P.sh ? P.sh - 1 : sy);
-  int r1 = sy + 1 < 0 ? 0 : (sy + 1 >= P.sh ? P.sh - 1 : sy + 1);
-  for (int c = 0; c < 3; c++) {
-    int h0, h1;
-    if (bx) {
-      h0 = S.at(r0, sx, c) * 2048;
-      h1 = S.at(r1, sx, c) * 2048;
-    } else {
-      h0 = S.at(r0, sx, c) * a0 + S.at(r0, sx + 1, c) * a1;
-      h1 = S.at(r1, sx, c) * a0 + S.at(r1, sx + 1, c) * a1;
-    }
-    int e = dx * 3 + c;
-    if (e < P.vec_end) {
-      int s0 = sat_s16i(h0 >> 4), s1 = sat_s16i(h1 >> 4);
-      int m0 = (s0 * (int)b0) >> 16, m1 = (s1 * (int)b1) >> 16;
-      int t = sat_s16i(m0 + m1);
-      out[c] = sat_u8i((t + 2) >> 2);
-    } else {
-      out[c] = sat_u8i((h0 * (int)b0 + h1 * (int)b1 + (1 << 21)) >> 22);
-    }
-  }
+  resize_linear(P, S, dx, lin_tap(P.scale_x, P.inv_x, P.sw, dx), lin_tap(P.scale_y, P.inv_y, P.sh, dy), out);
 }
 
 // Epilogue: flip (flip.py:35-40), cutout (cutout.py:44), LUT (normalize.py:65).

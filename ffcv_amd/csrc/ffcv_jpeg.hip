@@ -504,6 +504,7 @@ struct JpegArgs {
   uint32_t max_h, max_w;
   uint64_t max_blocks;
   uint64_t *dbg;
+  int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1248,47 +1249,55 @@ __global__ void __launch_bounds__(IDCT_T) jpeg_idct_kernel(JpegArgs a) {
 // K2: fancy upsampling + colour conversion into LDS, INTER_AREA + epilogue //
 // ======================================================================= //
 
+// Plane accessors: a component plane in HBM (GPlane) or a tile of it staged
+// in LDS (TPlane, rows [r0, ..] x cols [c0, ..] of the plane).
+struct GPlane {
+  const uint8_t *p;
+  int stride;
+  FFCV_DEV int at(int r, int c) const { return p[(uint64_t)r * stride + c]; }
+};
+struct TPlane {
+  const uint8_t *p;
+  int r0, c0, pitch;
+  FFCV_DEV int at(int r, int c) const { return p[(r - r0) * pitch + (c - c0)]; }
+};
+
 // jdsample.c upsampling of one component at full-resolution sample (y, x),
 // with libjpeg's context-row edge replication.
-FFCV_DEV int plane_at(const uint8_t *p, int stride, int ch, int y, int x) {
-  y = y < 0 ? 0 : (y >= ch ? ch - 1 : y);
-  return p[(uint64_t)y * stride + x];
-}
-FFCV_DEV int upsample_at(const uint8_t *p, int stride, int cw, int ch, int he, int ve, int y, int x) {
-  if (he == 1 && ve == 1) return p[(uint64_t)y * stride + x];
+template <class PL>
+FFCV_DEV int upsample_at(const PL &P, int cw, int ch, int he, int ve, int y, int x) {
+  auto clampr = [&](int r) { return r < 0 ? 0 : (r >= ch ? ch - 1 : r); };
+  if (he == 1 && ve == 1) return P.at(y, x);
   if (he == 2 && ve == 1) {
     int col = x >> 1;
-    const uint8_t *row = p + (uint64_t)y * stride;
-    if (cw <= 2) return row[col];
-    int cur = row[col] * 3;
+    if (cw <= 2) return P.at(y, col);
+    int cur = P.at(y, col) * 3;
     if (x & 1) {
-      if (col + 1 >= cw) return row[col];
-      return (cur + row[col + 1] + 2) >> 2;
+      if (col + 1 >= cw) return P.at(y, col);
+      return (cur + P.at(y, col + 1) + 2) >> 2;
     }
-    if (col == 0) return row[0];
-    return (cur + row[col - 1] + 1) >> 2;
+    if (col == 0) return P.at(y, 0);
+    return (cur + P.at(y, col - 1) + 1) >> 2;
   }
   if (he == 1 && ve == 2) {
     int r = y >> 1, other = (y & 1) ? r + 1 : r - 1;
-    int sum = plane_at(p, stride, ch, r, x) * 3 + plane_at(p, stride, ch, other, x);
+    int sum = P.at(clampr(r), x) * 3 + P.at(clampr(other), x);
     return (sum + ((y & 1) ? 2 : 1)) >> 2;
   }
   if (he == 2 && ve == 2) {
     int r = y >> 1, col = x >> 1;
-    if (cw <= 2) return p[(uint64_t)r * stride + col];
+    if (cw <= 2) return P.at(r, col);
     int other = (y & 1) ? r + 1 : r - 1;
-    int rc = r < 0 ? 0 : (r >= ch ? ch - 1 : r);
-    int oc = other < 0 ? 0 : (other >= ch ? ch - 1 : other);
-    const uint8_t *r0 = p + (uint64_t)rc * stride, *r1 = p + (uint64_t)oc * stride;
-    int thiss = r0[col] * 3 + r1[col];
+    int rc = clampr(r), oc = clampr(other);
+    int thiss = P.at(rc, col) * 3 + P.at(oc, col);
     if (x & 1) {
-      int nxt = col + 1 < cw ? r0[col + 1] * 3 + r1[col + 1] : thiss;
+      int nxt = col + 1 < cw ? P.at(rc, col + 1) * 3 + P.at(oc, col + 1) : thiss;
       return (thiss * 3 + nxt + 7) >> 4;
     }
-    int last = col > 0 ? r0[col - 1] * 3 + r1[col - 1] : thiss;
+    int last = col > 0 ? P.at(rc, col - 1) * 3 + P.at(oc, col - 1) : thiss;
     return (thiss * 3 + last + 8) >> 4;
   }
-  return p[(uint64_t)(y / ve) * stride + x / he];  // int_upsample
+  return P.at(y / ve, x / he);  // int_upsample
 }
 
 // jdcolor.c ycc_rgb_convert with build_ycc_rgb_table's fixed point
@@ -1299,15 +1308,34 @@ FFCV_DEV void ycc_rgb(int y, int cb, int cr, int out[3]) {
   out[2] = sat_u8i(y + ((116130 * x_cb + 32768) >> 16));
 }
 
-FFCV_DEV void pixel_rgb(const ImgInfo &I, const uint8_t *planes, int Y, int X, int v[3]) {
+// The per-image fields the colour pass needs, held in registers.
+struct ColorGeom {
+  int ncomp, color_rgb;
+  int he[3], ve[3], cw[3], ch[3];
+};
+FFCV_DEV ColorGeom color_geom(const ImgInfo &I) {
+  ColorGeom g;
+  g.ncomp = I.ncomp;
+  g.color_rgb = I.color_rgb;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    g.he[c] = I.he[c];
+    g.ve[c] = I.ve[c];
+    g.cw[c] = I.cw[c];
+    g.ch[c] = I.ch[c];
+  }
+  return g;
+}
+
+template <class PL>
+FFCV_DEV void pixel_rgb(const ColorGeom &I, const PL *pl, int Y, int X, int v[3]) {
   if (I.ncomp == 1) {
-    int g = planes[I.poff[0] + (uint64_t)Y * I.stride[0] + X];
-    v[0] = v[1] = v[2] = g;
+    v[0] = v[1] = v[2] = pl[0].at(Y, X);
     return;
   }
-  int s0 = upsample_at(planes + I.poff[0], I.stride[0], I.cw[0], I.ch[0], I.he[0], I.ve[0], Y, X);
-  int s1 = upsample_at(planes + I.poff[1], I.stride[1], I.cw[1], I.ch[1], I.he[1], I.ve[1], Y, X);
-  int s2 = upsample_at(planes + I.poff[2], I.stride[2], I.cw[2], I.ch[2], I.he[2], I.ve[2], Y, X);
+  int s0 = upsample_at(pl[0], I.cw[0], I.ch[0], I.he[0], I.ve[0], Y, X);
+  int s1 = upsample_at(pl[1], I.cw[1], I.ch[1], I.he[1], I.ve[1], Y, X);
+  int s2 = upsample_at(pl[2], I.cw[2], I.ch[2], I.he[2], I.ve[2], Y, X);
   if (I.color_rgb) {
     v[0] = s0;
     v[1] = s1;
@@ -1350,19 +1378,19 @@ template <int MODE, bool FP16>
 __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint16_t *s_lut = (uint16_t *)lds;  // 768 entries (FP16)
-  uint8_t *roi = lds + (FP16 ? 1536 : 0);
   const int t = threadIdx.x;
   const int k = blockIdx.y;
   const int band = blockIdx.x;
-  const ImgInfo I = a.info[k];
-  if (I.status == -1) return;  // raw sample (handled by the raw kernel)
+  const ImgInfo &I = a.info[k];
+  const int status = I.status;
+  if (status == -1) return;  // raw sample (handled by the raw kernel)
   const int out_h = MODE == JM_FULL ? (int)a.samples[k].height : a.p.out_h;
   const int out_w = MODE == JM_FULL ? (int)a.samples[k].width : a.p.out_w;
   const int oy0 = band * BAND, oy1 = min(out_h, oy0 + BAND);
   if (oy0 >= out_h) return;
   char *ob = (char *)a.out + a.out_stride * k;
   const int esz = FP16 ? 2 : 1;
-  if (I.status != FFCV_SAMPLE_OK) {  // zero-fill this band
+  if (status != FFCV_SAMPLE_OK) {  // zero-fill this band
     if (MODE == JM_RRC) {
       uint64_t row = (uint64_t)out_w * 3 * esz;
       for (uint64_t i = t; i < row * (oy1 - oy0); i += K2T) ob[row * oy0 + i] = 0;
@@ -1370,12 +1398,17 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
     return;
   }
   const uint8_t *planes = a.planes + a.plane_slot * k;
+  const ColorGeom G = color_geom(I);
+  const int ncomp = G.ncomp;
+  GPlane gp[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) gp[c] = GPlane{planes + I.poff[c], I.stride[c]};
   if (MODE == JM_FULL) {
     uint8_t *o = (uint8_t *)ob;
     for (int i = t; i < (oy1 - oy0) * out_w; i += K2T) {
       int y = oy0 + i / out_w, x = i % out_w;
       int v[3];
-      pixel_rgb(I, planes, y, x, v);
+      pixel_rgb(G, gp, y, x, v);
       uint8_t *d = o + ((uint64_t)y * out_w + x) * 3;
       d[0] = (uint8_t)v[0];
       d[1] = (uint8_t)v[1];
@@ -1385,25 +1418,94 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   }
   if (FP16)
     for (int i = t; i < 768; i += K2T) s_lut[i] = a.p.lut[i];
-  ResizePlan P = make_plan(I.rw, I.rh, out_w, out_h);
+  const int ri = I.ri, rj = I.rj, rh = I.rh, rw = I.rw;
+  ResizePlan P = make_plan(rw, rh, out_w, out_h);
   int r0, r1;
   band_rows(P, oy0, oy1, &r0, &r1);
   const int nrows = r1 - r0 + 1;
-  const int step = I.rw * 3;
-  const bool staged = (uint64_t)nrows * step <= (uint64_t)(K2_LDS - (FP16 ? 1536 : 0));
-  // Bands too wide for LDS stage their rows in the image's coefficient slot
-  // (dead once K1 has run) at their absolute crop-row position; rows shared
-  // with a neighbouring band are written with identical bytes by both.
+  const int step = rw * 3;
+  // LDS: [LUT][column + row taps][component tiles][RGB rows].  The taps of
+  // the band's rows and of every output column are computed once per
+  // workgroup; the tiles cover every plane sample the band's upsampling
+  // reads, so the colour pass runs from LDS.
+  const int tap_b = (P.kind == 2 ? (int)sizeof(AreaTaps) : (P.kind == 3 ? (int)sizeof(LinTap) : 0)) * (out_w + BAND);
+  const int lut_b = (FP16 ? 1536 : 0) + ((tap_b + 15) & ~15);
+  AreaTaps *atab = (AreaTaps *)(lds + (FP16 ? 1536 : 0));
+  LinTap *ltab = (LinTap *)atab;
+  int ty0[3], tx0[3], trows[3], tcols[3], toff[3];
+  int need = lut_b;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {  // (unrolled: no dynamically indexed arrays)
+    if (c >= ncomp) {
+      ty0[c] = tx0[c] = trows[c] = tcols[c] = toff[c] = 0;
+      continue;
+    }
+    const int he = G.he[c], ve = G.ve[c];
+    int y0 = (ri + r0) / ve - (ve == 2 ? 1 : 0), y1 = (ri + r1) / ve + (ve == 2 ? 1 : 0);
+    int x0 = rj / he - (he == 2 ? 1 : 0), x1 = (rj + rw - 1) / he + (he == 2 ? 1 : 0);
+    y0 = max(y0, 0);
+    x0 = max(x0, 0);
+    y1 = min(y1, G.ch[c] - 1);
+    x1 = min(x1, G.cw[c] - 1);
+    ty0[c] = y0;
+    tx0[c] = x0;
+    trows[c] = y1 - y0 + 1;
+    tcols[c] = x1 - x0 + 1;
+    toff[c] = need;
+    need += (trows[c] * tcols[c] + 15) & ~15;
+  }
+  const int roi_off = need;
+  need += nrows * step;
+  const bool tiled = need <= K2_LDS && !(a.k2flags & 1);
+  const bool staged = tiled || lut_b + nrows * step <= K2_LDS;  // (tap tables fit: see tabs)
+  uint8_t *roi = lds + (tiled ? roi_off : lut_b);
+  // Bands too wide for LDS stage their rows in the image's rgb slot at their
+  // absolute crop-row position; rows shared with a neighbouring band are
+  // written with identical bytes by both.
   uint8_t *groi = a.rgb + a.plane_slot * k;
   uint8_t *dst = staged ? roi : groi + (uint64_t)r0 * step;
-  for (int i = t; i < nrows * I.rw; i += K2T) {
-    int yy = i / I.rw, x = i - yy * I.rw;
-    int v[3];
-    pixel_rgb(I, planes, I.ri + r0 + yy, I.rj + x, v);
-    uint8_t *d = dst + (uint64_t)yy * step + x * 3;
-    d[0] = (uint8_t)v[0];
-    d[1] = (uint8_t)v[1];
-    d[2] = (uint8_t)v[2];
+  const bool tabs = tap_b > 0 && lut_b <= K2_LDS / 2 && !(a.k2flags & 2);
+  if (tabs) {  // [0, out_w): columns, [out_w, out_w + rows): the band's rows
+    for (int i = t; i < out_w + (oy1 - oy0); i += K2T) {
+      if (P.kind == 2)
+        atab[i] = i < out_w ? area_taps(P.sw, P.scale_x, i) : area_taps(P.sh, P.scale_y, oy0 + i - out_w);
+      else
+        ltab[i] = i < out_w ? lin_tap(P.scale_x, P.inv_x, P.sw, i) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + i - out_w);
+    }
+  }
+  if (tiled) {
+    TPlane tp[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      uint8_t *tl = lds + toff[c];
+      const int cols = tcols[c], n = trows[c] * cols;
+      const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
+      for (int i = t; i < n; i += K2T) {
+        const int rr = i / cols, cc = i - rr * cols;
+        tl[rr * cols + cc] = src[(uint64_t)rr * gp[c].stride + cc];
+      }
+      tp[c] = TPlane{tl, ty0[c], tx0[c], cols};
+    }
+    __syncthreads();
+    for (int i = t; i < nrows * rw; i += K2T) {
+      int yy = i / rw, x = i - yy * rw;
+      int v[3];
+      pixel_rgb(G, tp, ri + r0 + yy, rj + x, v);
+      uint8_t *d = dst + yy * step + x * 3;
+      d[0] = (uint8_t)v[0];
+      d[1] = (uint8_t)v[1];
+      d[2] = (uint8_t)v[2];
+    }
+  } else {
+    for (int i = t; i < nrows * rw; i += K2T) {
+      int yy = i / rw, x = i - yy * rw;
+      int v[3];
+      pixel_rgb(G, gp, ri + r0 + yy, rj + x, v);
+      uint8_t *d = dst + (uint64_t)yy * step + x * 3;
+      d[0] = (uint8_t)v[0];
+      d[1] = (uint8_t)v[1];
+      d[2] = (uint8_t)v[2];
+    }
   }
   __syncthreads();
   Epilogue ep;
@@ -1419,30 +1521,62 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   ep.fill[2] = a.p.cutout_fill[2];
   LdsRoi lr{roi, r0, step};
   RoiSrc gr{groi, (uint64_t)step};
-  const int npx = (oy1 - oy0) * out_w;
-  for (int i = t; i < npx; i += K2T) {
-    int dy = oy0 + i / out_w, dx = i % out_w;
-    int v[3];
+  auto px = [&](int dy, int dx, int v[3]) {
     if (ep.in_cut(dy, dx)) {
       v[0] = ep.fill[0];
       v[1] = ep.fill[1];
       v[2] = ep.fill[2];
+    } else if (staged && tabs) {
+      const int cx = ep.src_x(dx);
+      if (P.kind == 2)
+        resize_area(lr, atab[cx], atab[out_w + dy - oy0], v);
+      else
+        resize_linear(P, lr, cx, ltab[cx], ltab[out_w + dy - oy0], v);
     } else if (staged) {
       resize_pixel(P, lr, dy, ep.src_x(dx), v);
     } else {
       resize_pixel(P, gr, dy, ep.src_x(dx), v);
     }
-    uint64_t px = (uint64_t)dy * out_w + dx;
+  };
+  // pixel pairs: 12 bytes (fp16) / 6 bytes (u8) per thread, 4-/2-byte
+  // aligned when rows and samples start aligned; single pixels otherwise
+  const bool pairs = (out_w & 1) == 0 && (a.out_stride & 3) == 0 && !(a.k2flags & 4);
+  const int per = pairs ? 2 : 1;
+  const int hw = out_w / per;
+  const int npx = (oy1 - oy0) * hw;
+  for (int i = t; i < npx; i += K2T) {
+    const int dy = oy0 + i / hw, dx = per * (i % hw);
+    const bool two = pairs;
+    int v[3], u[3];
+    px(dy, dx, v);
+    if (two) px(dy, dx + 1, u);
+    const uint64_t p0 = (uint64_t)dy * out_w + dx;
     if (FP16) {
-      uint16_t *o = (uint16_t *)ob + px * 3;
-      o[0] = s_lut[v[0] * 3];
-      o[1] = s_lut[v[1] * 3 + 1];
-      o[2] = s_lut[v[2] * 3 + 2];
+      uint16_t h0 = s_lut[v[0] * 3], h1 = s_lut[v[1] * 3 + 1], h2 = s_lut[v[2] * 3 + 2];
+      uint16_t *o = (uint16_t *)ob + p0 * 3;
+      if (two) {
+        uint16_t h3 = s_lut[u[0] * 3], h4 = s_lut[u[1] * 3 + 1], h5 = s_lut[u[2] * 3 + 2];
+        uint32_t *o32 = (uint32_t *)o;  // p0 even -> 12-byte aligned group
+        o32[0] = h0 | ((uint32_t)h1 << 16);
+        o32[1] = h2 | ((uint32_t)h3 << 16);
+        o32[2] = h4 | ((uint32_t)h5 << 16);
+      } else {
+        o[0] = h0;
+        o[1] = h1;
+        o[2] = h2;
+      }
     } else {
-      uint8_t *o = (uint8_t *)ob + px * 3;
-      o[0] = (uint8_t)v[0];
-      o[1] = (uint8_t)v[1];
-      o[2] = (uint8_t)v[2];
+      uint8_t *o = (uint8_t *)ob + p0 * 3;
+      if (two) {
+        uint16_t *o16 = (uint16_t *)o;
+        o16[0] = (uint16_t)(v[0] | (v[1] << 8));
+        o16[1] = (uint16_t)(v[2] | (u[0] << 8));
+        o16[2] = (uint16_t)(u[1] | (u[2] << 8));
+      } else {
+        o[0] = (uint8_t)v[0];
+        o[1] = (uint8_t)v[1];
+        o[2] = (uint8_t)v[2];
+      }
     }
   }
 }
@@ -1548,6 +1682,8 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.max_h = c->max_h;
   a.max_w = c->max_w;
   a.dbg = c->dbg;
+  const char *f = getenv("FFCV_K2_FLAGS");  // diagnostics only
+  a.k2flags = f ? atoi(f) : 0;
   return a;
 }
 

@@ -303,12 +303,26 @@ def main():
                    'parallelism': f'dp{world} (traversal-order sharding, no collectives)'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': None,
-                     'kernel': ('jpeg_entropy_kernel<RRC> + jpeg_color_resize_kernel<RRC,fp16> (one decode launch pair)'
+                     'kernel': ('jpeg_entropy_kernel<RRC> + jpeg_idct_kernel + jpeg_color_resize_kernel<RRC,fp16> '
+                                '(one decode launch sequence, HIP events on the slot stream)'
                                 if mode == 'jpg' else 'rrc_raw_kernel'),
                      'kernel_ms': round(kern_ms, 4), 'algorithmic_bytes_per_image': round(unit_bytes, 1),
                      'note': roof_note},
         'cpu_baseline': None,
     }
+    # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
+    # (tools/profile.sh -> tools/pmc_summary.py), per launch like `achieved`
+    prof = os.path.join(ROOT, 'profiles', f'traffic_{args.config}.json')
+    if os.path.exists(prof):
+        pm = json.load(open(prof))
+        names = (['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', 'jpeg_color_resize_kernel<0, true>']
+                 if mode == 'jpg' else ['rrc_raw_kernel<false>'])
+        if all(n in pm and 'fetch_size_kb' in pm[n] and 'write_size_kb' in pm[n] for n in names):
+            tb = sum((pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 for n in names)
+            res['roofline']['traffic'] = round(tb, 1)
+            res['roofline']['traffic_note'] = (f'bytes per launch (FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC, '
+                                               f'profiles/traffic_{args.config}.json); algorithmic '
+                                               f'{unit_bytes * batch:.0f}')
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(args.config, tile, offs, sizes, hs, ws, args.cpu_budget)
     if rank == 0:

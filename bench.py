@@ -143,11 +143,19 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
+    # one process per GPU; FFCV_BENCH_BACKEND=gloo + several ranks per GPU
+    # (local % device_count) only rehearse the N>1 path on a 1-GPU box
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev
+    backend = os.environ.get('FFCV_BENCH_BACKEND', 'nccl')
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
+        torch.cuda.set_device(gpu)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device('cuda', gpu)
     torch.cuda.set_device(dev)
 
     from ffcv_amd import _build
@@ -270,7 +278,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

@@ -1642,7 +1642,10 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
       // the entropy kernel writes only non-zero coefficients into an
       // all-zero slot; the IDCT kernel restores the zeros it consumed
-      (e = hipMemset(c->coef, 0, c->coef_slot * 2 * max_batch)) != hipSuccess) {
+      (e = hipMemset(c->coef, 0, c->coef_slot * 2 * max_batch)) != hipSuccess ||
+      // the memset runs on the null stream, which does not order non-blocking
+      // streams (torch's): finish it before any launch can use the context
+      (e = hipDeviceSynchronize()) != hipSuccess) {
     int rc = ffcv::check_hip(e, "ffcv_jpeg_create: hipMalloc");
     free_ctx(c);
     return rc;

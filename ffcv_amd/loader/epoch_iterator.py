@@ -12,6 +12,8 @@ status codes are copied back asynchronously and checked without stalling
 the pipeline (a corrupt or unsupported JPEG raises FFCVError; the reference
 silently returns garbage, rgb_image.py:131,196).
 """
+import os
+import time
 from queue import Queue, Full
 from threading import Thread, Event
 
@@ -25,6 +27,9 @@ from ..utils import chunks
 
 class DecodeError(RuntimeError):
     pass
+
+
+MAX_STREAMS = 3
 
 
 class EpochIterator(Thread):
@@ -52,16 +57,54 @@ class EpochIterator(Thread):
             raise e
         self.storage_state = self.memory_context.state
         n_slots = self.loader.batches_ahead + 2
-        self.cuda_streams = [(ch.cuda.Stream(self.device) if self.is_cuda else None)
-                             for _ in range(n_slots)]
-        self.memory_allocations = self.loader.graph.allocate_memory(self.loader.batch_size, n_slots)
-        self.contexts = [runtime.BatchContext(self.storage_state, loader.device_dataset, loader.seed,
-                                              s, loader.batch_size) for s in range(n_slots)]
+        # Slot state lives on the loader across epochs: the device buffers and
+        # the JPEG decoder scratch (hundreds of MB per slot) are allocated
+        # once, not per epoch.  The slots share at most MAX_STREAMS HIP
+        # streams (slot % MAX_STREAMS; two slots on one stream are simply
+        # ordered), so the slot streams plus the consumer's fit the GPU's
+        # hardware queues (GPU_MAX_HW_QUEUES defaults to 4).
+        key = (n_slots, self.loader.batch_size)
+        cache = getattr(loader, '_slot_cache', None)
+        if cache is None or cache['key'] != key:
+            streams = [(ch.cuda.Stream(self.device) if self.is_cuda else None)
+                       for _ in range(min(n_slots, MAX_STREAMS))]
+            cache = {'key': key,
+                     'streams': [streams[s % len(streams)] for s in range(n_slots)],
+                     'memory': self.loader.graph.allocate_memory(self.loader.batch_size, n_slots),
+                     'contexts': [runtime.BatchContext(None, loader.device_dataset, loader.seed, s,
+                                                       loader.batch_size) for s in range(n_slots)]}
+            loader._slot_cache = cache
+        self.cuda_streams = cache['streams']
+        self.memory_allocations = cache['memory']
+        self.contexts = cache['contexts']
+        for c in self.contexts:
+            c.host_state = self.storage_state
+            c.loader_seed = loader.seed
+        if self.is_cuda:  # reused buffers: order this epoch after the consumer's queued work
+            ev = ch.cuda.Event()
+            ev.record(self.current_stream)
+            for st in set(self.cuda_streams):
+                st.wait_event(ev)
         self._status = [None] * n_slots
+        self._t_pipeline = 0.0  # host seconds spent enqueueing batches (FFCV_LOADER_TIMING=1 prints it)
         self.start()
 
     # ------------------------------------------------------------- thread --
     def run(self):
+        if os.environ.get('FFCV_LOADER_PROFILE'):  # diagnostics: cProfile of the producer thread
+            import cProfile
+            import pstats
+            prof = cProfile.Profile()
+            prof.enable()
+            try:
+                self._run()
+            finally:
+                prof.disable()
+                pstats.Stats(prof).sort_stats('tottime').print_stats(25)
+            return
+        self._run()
+
+    def _run(self):
         events = [None for _ in self.cuda_streams]
         try:
             b_ix = 0
@@ -70,7 +113,9 @@ class EpochIterator(Thread):
                 ixes = next(self.iter_ixes)
                 slot = self.current_batch_slot
                 self.current_batch_slot = (slot + 1) % (self.loader.batches_ahead + 2)
+                t0 = time.perf_counter()
                 result = self.run_pipeline(b_ix, ixes, slot, events[slot])
+                self._t_pipeline += time.perf_counter() - t0
                 to_output = (slot, result)
                 while True:
                     try:
@@ -87,6 +132,9 @@ class EpochIterator(Thread):
                     events[just_finished_slot] = event
                 b_ix += 1
         except StopIteration:
+            if os.environ.get('FFCV_LOADER_TIMING'):
+                print(f'# epoch {self.epoch}: {b_ix} batches, host enqueue {self._t_pipeline * 1e3 / max(1, b_ix):.3f} '
+                      f'ms/batch', flush=True)
             self.output_queue.put(None)
         except BaseException as e:  # surface worker errors to the consumer
             self.error = e

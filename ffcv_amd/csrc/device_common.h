@@ -394,6 +394,28 @@ FFCV_DEV void resize_pixel(const ResizePlan &P, const Src &S, int dy, int dx, in
   resize_linear(P, S, dx, lin_tap(P.scale_x, P.inv_x, P.sw, dx), lin_tap(P.scale_y, P.inv_y, P.sh, dy), out);
 }
 
+// Source rows of the crop that output rows [oy0, oy1) read.
+FFCV_DEV void band_rows(const ResizePlan &P, int oy0, int oy1, int *r0, int *r1) {
+  if (P.kind == 0) {
+    *r0 = oy0;
+    *r1 = oy1 - 1;
+  } else if (P.kind == 1) {
+    *r0 = oy0 * P.isy;
+    *r1 = oy1 * P.isy - 1;
+  } else if (P.kind == 2) {
+    AreaTaps a = area_taps(P.sh, P.scale_y, oy0);
+    AreaTaps b = area_taps(P.sh, P.scale_y, oy1 - 1);
+    *r0 = a.lo;
+    *r1 = b.hi;
+  } else {
+    int s0 = (int)floor(oy0 * P.scale_y), s1 = (int)floor((oy1 - 1) * P.scale_y) + 1;
+    *r0 = s0;
+    *r1 = s1;
+  }
+  *r0 = min(max(*r0, 0), P.sh - 1);
+  *r1 = min(max(*r1, 0), P.sh - 1);
+}
+
 // Epilogue: flip (flip.py:35-40), cutout (cutout.py:44), LUT (normalize.py:65).
 // Returns the source x to resize for output column dx, and whether the
 // output pixel is inside the cutout square.

@@ -1352,28 +1352,6 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
   FFCV_DEV int at(int y, int x, int c) const { return p[(y - row0) * step + x * 3 + c]; }
 };
 
-// Source rows of the crop that output rows [oy0, oy1) read.
-FFCV_DEV void band_rows(const ResizePlan &P, int oy0, int oy1, int *r0, int *r1) {
-  if (P.kind == 0) {
-    *r0 = oy0;
-    *r1 = oy1 - 1;
-  } else if (P.kind == 1) {
-    *r0 = oy0 * P.isy;
-    *r1 = oy1 * P.isy - 1;
-  } else if (P.kind == 2) {
-    AreaTaps a = area_taps(P.sh, P.scale_y, oy0);
-    AreaTaps b = area_taps(P.sh, P.scale_y, oy1 - 1);
-    *r0 = a.lo;
-    *r1 = b.hi;
-  } else {
-    int s0 = (int)floor(oy0 * P.scale_y), s1 = (int)floor((oy1 - 1) * P.scale_y) + 1;
-    *r0 = s0;
-    *r1 = s1;
-  }
-  *r0 = min(max(*r0, 0), P.sh - 1);
-  *r1 = min(max(*r1, 0), P.sh - 1);
-}
-
 template <int MODE, bool FP16>
 __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];

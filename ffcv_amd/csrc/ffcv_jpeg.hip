@@ -504,7 +504,9 @@ struct JpegArgs {
   uint32_t max_h, max_w;
   uint64_t max_blocks;
   uint64_t *dbg;
-  int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs
+  int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs;
+                // timing only (wrong output): bit 3 skips the colour pass, bit 4 the resize arithmetic;
+                // bit 5 disables the separable linear resize
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1465,7 +1467,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       tp[c] = TPlane{tl, ty0[c], tx0[c], cols};
     }
     __syncthreads();
-    for (int i = t; i < nrows * rw; i += K2T) {
+    for (int i = t; i < (a.k2flags & 8 ? 0 : nrows * rw); i += K2T) {
       int yy = i / rw, x = i - yy * rw;
       int v[3];
       pixel_rgb(G, tp, ri + r0 + yy, rj + x, v);
@@ -1485,7 +1487,30 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       d[2] = (uint8_t)v[2];
     }
   }
+  // Separable linear (kind 3): OpenCV's horizontal pass depends only on the
+  // source row, so each (row, column) tap pair is computed once per band and
+  // kept as the saturated int16 (h >> 4) the vertical SIMD body consumes
+  // (resize.cpp VResizeLinearVec_32s8u).  Columns in the scalar tail
+  // (>= vec_end) keep the per-pixel path.
+  const int hoff = (((tiled ? roi_off : lut_b) + nrows * step) + 15) & ~15;
+  const bool sep = P.kind == 3 && staged && tabs && hoff + nrows * out_w * 8 <= K2_LDS && !(a.k2flags & 32);
+  uint2 *H = (uint2 *)(lds + hoff);
   __syncthreads();
+  if (sep) {
+    for (int i = t; i < nrows * out_w; i += K2T) {
+      const int rr = i / out_w, cx = i - rr * out_w;
+      const LinTap lx = ltab[cx];
+      const uint8_t *q = roi + rr * step + lx.s * 3;
+      int hv[3];
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const int h = lx.border ? q[c] * 2048 : q[c] * lx.c0 + q[c + 3] * lx.c1;
+        hv[c] = sat_s16i(h >> 4);
+      }
+      H[i] = make_uint2((uint32_t)(hv[0] & 0xffff) | ((uint32_t)hv[1] << 16), (uint32_t)(hv[2] & 0xffff));
+    }
+    __syncthreads();
+  }
   Epilogue ep;
   ep.out_h = out_h;
   ep.out_w = out_w;
@@ -1504,6 +1529,22 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       v[0] = ep.fill[0];
       v[1] = ep.fill[1];
       v[2] = ep.fill[2];
+    } else if (a.k2flags & 16) {
+      v[0] = lr.p[dx];
+      v[1] = lr.p[dx + 1];
+      v[2] = lr.p[dx + 2];
+    } else if (sep && ep.src_x(dx) * 3 + 2 < P.vec_end) {
+      const int cx = ep.src_x(dx);
+      const LinTap ly = ltab[out_w + dy - oy0];
+      const int ra = min(max(ly.s, 0), P.sh - 1) - r0, rb = min(max(ly.s + 1, 0), P.sh - 1) - r0;
+      const uint2 A = H[ra * out_w + cx], Bv = H[rb * out_w + cx];
+      const int a0[3] = {(int16_t)(A.x & 0xffff), (int16_t)(A.x >> 16), (int16_t)(A.y & 0xffff)};
+      const int b0[3] = {(int16_t)(Bv.x & 0xffff), (int16_t)(Bv.x >> 16), (int16_t)(Bv.y & 0xffff)};
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const int m0 = (a0[c] * ly.c0) >> 16, m1 = (b0[c] * ly.c1) >> 16;
+        v[c] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
+      }
     } else if (staged && tabs) {
       const int cx = ep.src_x(dx);
       if (P.kind == 2)

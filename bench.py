@@ -33,6 +33,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# 16 HIP hardware queues so --inflight 8 batches run on 8 streams that do not
+# share queues (HIP's default is 4; see ffcv_amd/__init__.py).
+os.environ.setdefault('GPU_MAX_HW_QUEUES', '16')
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 CONFIGS = {
@@ -134,7 +138,7 @@ def main():
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)
-    ap.add_argument('--inflight', type=int, default=3,
+    ap.add_argument('--inflight', type=int, default=8,
                     help='batches in flight on separate HIP streams (Loader batches_ahead analogue)')
     args = ap.parse_args()
 

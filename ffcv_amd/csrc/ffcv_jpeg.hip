@@ -506,7 +506,7 @@ struct JpegArgs {
   uint64_t *dbg;
   int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs;
                 // timing only (wrong output): bit 3 skips the colour pass, bit 4 the resize arithmetic;
-                // bit 5 disables the separable linear resize
+                // bit 5 disables the separable linear resize, bit 6 the 4:2:0 quad colour pass
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1347,6 +1347,24 @@ FFCV_DEV void pixel_rgb(const ColorGeom &I, const PL *pl, int Y, int X, int v[3]
   }
 }
 
+// h2v2 fancy upsampling (jdsample.c h2v2_fancy_upsample) of the 2x2 output
+// quad that chroma sample (R, C) expands to: q[0..3] = (2R,2C), (2R,2C+1),
+// (2R+1,2C), (2R+1,2C+1).  Same arithmetic as upsample_at(he=ve=2, cw>2),
+// with the 3x3 neighbourhood read once.
+template <class PL>
+FFCV_DEV void upsample_quad_h2v2(const PL &P, int cw, int ch, int R, int C, int q[4]) {
+  const int ru = max(R - 1, 0), rd = min(R + 1, ch - 1);
+  const int cl = max(C - 1, 0), cr = min(C + 1, cw - 1);
+  const int ml = P.at(R, cl), mc = P.at(R, C), mr = P.at(R, cr);
+  const int tl = 3 * ml + P.at(ru, cl), tc = 3 * mc + P.at(ru, C), tr = 3 * mr + P.at(ru, cr);
+  const int bl = 3 * ml + P.at(rd, cl), bc = 3 * mc + P.at(rd, C), br = 3 * mr + P.at(rd, cr);
+  const bool first = C == 0, last = C + 1 >= cw;
+  q[0] = (3 * tc + (first ? tc : tl) + 8) >> 4;
+  q[1] = (3 * tc + (last ? tc : tr) + 7) >> 4;
+  q[2] = (3 * bc + (first ? bc : bl) + 8) >> 4;
+  q[3] = (3 * bc + (last ? bc : br) + 7) >> 4;
+}
+
 struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
   const uint8_t *p;
   int row0;
@@ -1467,14 +1485,41 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       tp[c] = TPlane{tl, ty0[c], tx0[c], cols};
     }
     __syncthreads();
-    for (int i = t; i < (a.k2flags & 8 ? 0 : nrows * rw); i += K2T) {
-      int yy = i / rw, x = i - yy * rw;
-      int v[3];
-      pixel_rgb(G, tp, ri + r0 + yy, rj + x, v);
-      uint8_t *d = dst + yy * step + x * 3;
-      d[0] = (uint8_t)v[0];
-      d[1] = (uint8_t)v[1];
-      d[2] = (uint8_t)v[2];
+    const bool q420 = ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 &&
+                      G.ve[1] == 2 && G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2 &&
+                      !(a.k2flags & 64);
+    if (a.k2flags & 8) {
+    } else if (q420) {  // one thread per chroma sample: a 2x2 quad of pixels
+      const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
+      const int R0 = Y0 >> 1, C0 = X0 >> 1, qcols = (X1 >> 1) - C0 + 1;
+      const int nq = ((Y1 >> 1) - R0 + 1) * qcols;
+      for (int i = t; i < nq; i += K2T) {
+        const int qr = i / qcols, R = R0 + qr, C = C0 + (i - qr * qcols);
+        int cb[4], cr[4];
+        upsample_quad_h2v2(tp[1], G.cw[1], G.ch[1], R, C, cb);
+        upsample_quad_h2v2(tp[2], G.cw[2], G.ch[2], R, C, cr);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int Y = 2 * R + (u >> 1), X = 2 * C + (u & 1);
+          if (Y < Y0 || Y > Y1 || X < X0 || X > X1) continue;
+          int v[3];
+          ycc_rgb(tp[0].at(Y, X), cb[u], cr[u], v);
+          uint8_t *d = dst + (Y - Y0) * step + (X - X0) * 3;
+          d[0] = (uint8_t)v[0];
+          d[1] = (uint8_t)v[1];
+          d[2] = (uint8_t)v[2];
+        }
+      }
+    } else {
+      for (int i = t; i < nrows * rw; i += K2T) {
+        int yy = i / rw, x = i - yy * rw;
+        int v[3];
+        pixel_rgb(G, tp, ri + r0 + yy, rj + x, v);
+        uint8_t *d = dst + yy * step + x * 3;
+        d[0] = (uint8_t)v[0];
+        d[1] = (uint8_t)v[1];
+        d[2] = (uint8_t)v[2];
+      }
     }
   } else {
     for (int i = t; i < nrows * rw; i += K2T) {

@@ -29,7 +29,14 @@ class DecodeError(RuntimeError):
     pass
 
 
-MAX_STREAMS = 3
+def max_streams():
+    """Slot streams the Loader may use: one hardware queue stays free for the
+    consumer's stream, and more than 8 concurrent batches measured slower."""
+    try:
+        hwq = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+    except ValueError:
+        hwq = 4
+    return max(1, min(8, hwq - 1))
 
 
 class EpochIterator(Thread):
@@ -59,15 +66,15 @@ class EpochIterator(Thread):
         n_slots = self.loader.batches_ahead + 2
         # Slot state lives on the loader across epochs: the device buffers and
         # the JPEG decoder scratch (hundreds of MB per slot) are allocated
-        # once, not per epoch.  The slots share at most MAX_STREAMS HIP
-        # streams (slot % MAX_STREAMS; two slots on one stream are simply
-        # ordered), so the slot streams plus the consumer's fit the GPU's
-        # hardware queues (GPU_MAX_HW_QUEUES defaults to 4).
+        # once, not per epoch.  The slots share at most max_streams() HIP
+        # streams (slot % n; two slots on one stream are simply ordered), so
+        # the slot streams plus the consumer's fit the GPU's hardware queues
+        # (GPU_MAX_HW_QUEUES, raised to 16 by ffcv_amd/__init__.py).
         key = (n_slots, self.loader.batch_size)
         cache = getattr(loader, '_slot_cache', None)
         if cache is None or cache['key'] != key:
             streams = [(ch.cuda.Stream(self.device) if self.is_cuda else None)
-                       for _ in range(min(n_slots, MAX_STREAMS))]
+                       for _ in range(min(n_slots, max_streams()))]
             cache = {'key': key,
                      'streams': [streams[s % len(streams)] for s in range(n_slots)],
                      'memory': self.loader.graph.allocate_memory(self.loader.batch_size, n_slots),

@@ -6,7 +6,7 @@
 # with tracing domains; MI355X_MICROARCH.md rocprofv3 section).
 set -e
 TAG=${1:-r1}; shift || true
-ARGS=${@:---dataset-size 262144 --steps 30 --warmup 5 --no-cpu-baseline --inflight 3}
+ARGS=${@:---dataset-size 262144 --steps 30 --warmup 5 --no-cpu-baseline --inflight 8}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

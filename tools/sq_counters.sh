@@ -4,7 +4,7 @@
 # Two PMC passes (8 SQ slots each), no tracing domains combined with --pmc.
 set -e
 TAG=${1:-sq}; shift || true
-ARGS=${@:---dataset-size 65536 --steps 10 --warmup 3 --no-cpu-baseline --inflight 3}
+ARGS=${@:---dataset-size 65536 --steps 10 --warmup 3 --no-cpu-baseline --inflight 8}
 OUT=gpurun_out/sq_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

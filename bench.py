@@ -33,8 +33,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# 16 HIP hardware queues so --inflight 8 batches run on 8 streams that do not
-# share queues (HIP's default is 4; see ffcv_amd/__init__.py).
+# 16 HIP hardware queues so the --inflight batches' streams do not share a
+# queue (HIP's default is 4; more than 16 measured far slower: time-sliced
+# queues; see ffcv_amd/__init__.py).
 os.environ.setdefault('GPU_MAX_HW_QUEUES', '16')
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -138,7 +139,9 @@ def main():
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)
-    ap.add_argument('--inflight', type=int, default=8,
+    ap.add_argument('--only', type=int, default=0,
+                    help='diagnostic: timed steps launch only these decode kernels (bit 0 K1, 1 K1b, 2 K2)')
+    ap.add_argument('--inflight', type=int, default=16,
                     help='batches in flight on separate HIP streams (Loader batches_ahead analogue)')
     args = ap.parse_args()
 
@@ -270,6 +273,8 @@ def main():
             assert (st == 0).all(), f'decode status {np.unique(st)}'
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
+    if args.only:
+        os.environ['FFCV_JPEG_ONLY'] = str(args.only)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

@@ -71,6 +71,9 @@
 #define BAND 16
 #define K2T 256
 #define K2_LDS 49152
+#ifndef JW
+#define JW 4  // images (waves) per K1 workgroup
+#endif
 
 enum JMode { JM_RRC = 0, JM_FULL = 1, JM_COEF = 2 };
 
@@ -89,6 +92,25 @@ struct ImgInfo {
   int16_t qmul[3][64];
 };
 
+// Huffman decode tables built from one image's DHT segments.  K1 runs JW
+// images per workgroup; images whose tables (and table slots) are byte-
+// identical to the workgroup's first valid image share ONE LDS copy -- the
+// usual case, every encoder of a dataset writes the same tables -- and any
+// other image builds its own copy in global scratch (L1/L2-resident).
+struct JTables {
+  uint32_t lim[NSLOT][17];  // left-justified end of length-l codes
+  int32_t valoff[NSLOT][17];
+  uint8_t vals[NSLOT][256];
+  int nsub[NSLOT];
+  int nvals[NSLOT];
+  int bad;
+  uint16_t sub_prefix[NSLOT][NSUB];
+  // second-level tables (codes longer than the first level; make_entry format)
+  uint16_t lut2[NLUTSLOT][NSUB][1 << SUBB];
+  uint16_t lut[LUT_POOL];  // first-level LUT pool
+};
+
+// Per-image (per-wave) state.
 struct JShared {
   int status;
   int W, H, ncomp, hmax, vmax;
@@ -121,24 +143,16 @@ struct JShared {
   // in its component's plane, blocks per MCU row step, hs, and the window
   // as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
   int4 pdesc[10][2];
-  // decode tables
-  uint32_t lim[NSLOT][17];  // left-justified end of length-l codes
-  int32_t valoff[NSLOT][17];
-  uint8_t vals[NSLOT][256];
-  int nsub[NSLOT];
-  int nvals[NSLOT];
-  uint16_t sub_prefix[NSLOT][NSUB];
-  // second-level tables (codes longer than the first level; make_entry format)
-  uint16_t lut2[NLUTSLOT][NSUB][1 << SUBB];
   union {
+    uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
     uint32_t ev[2][NEV + 1][JT];  // P3: block-start events (pos << 4 | phase), double-buffered
     uint8_t stage[2 * (NEV + 1) * JT * 4];  // P2: de-stuffed bytes awaiting a flush
   };
-  // header bytes, then the first-level LUT pool (same storage)
-  union {
-    uint8_t hdr[HDR_BYTES];
-    uint16_t lut[LUT_POOL];
-  } u;
+};
+
+struct K1Shared {
+  JTables tab;
+  JShared w[JW];
 };
 
 // zigzag index of each natural (row-major) coefficient position; the entropy
@@ -223,26 +237,28 @@ FFCV_DEV uint32_t make_entry(bool ac, int len, int sym) {
 // Canonical decode of a 16-bit lookahead (jdhuff.c jpeg_huff_decode): the
 // code length is the first l with look < lim[l]; past lim[16] the code is
 // invalid and, like libjpeg, yields symbol 0 after 16 bits.
-FFCV_DEV uint32_t slow_entry(const JShared &S, int slot, uint32_t look) {
+template <class TB>
+FFCV_DEV uint32_t slow_entry(const TB &T, uint32_t acmask, int slot, uint32_t look) {
   int len = 1;
 #pragma unroll
-  for (int l = 1; l < 16; l++) len += look >= S.lim[slot][l];
+  for (int l = 1; l < 16; l++) len += look >= T.lim[slot][l];
   int sym = 0;
-  if (look < S.lim[slot][16]) sym = S.vals[slot][(S.valoff[slot][len] + (int)(look >> (16 - len))) & 0xff];
+  if (look < T.lim[slot][16]) sym = T.vals[slot][(T.valoff[slot][len] + (int)(look >> (16 - len))) & 0xff];
   else len = 16;
-  return make_entry((S.acmask >> slot) & 1, len, sym);
+  return make_entry((acmask >> slot) & 1, len, sym);
 }
 
 // inf = sinfo of the table: LUT base | bits << 16 | slot << 20 | second-
 // level set << 23.  A slot without a first-level LUT (bits 0) points at a
 // reserved zero word.
-FFCV_DEV uint32_t decode_entry(const JShared &S, uint32_t inf, uint64_t acc) {
+template <class TB>
+FFCV_DEV uint32_t decode_entry(const TB &T, uint32_t acmask, uint32_t inf, uint64_t acc) {
   const uint32_t look = (uint32_t)(acc >> 48);
   const int bits = (int)((inf >> 16) & 15), slot = (int)((inf >> 20) & 7);
-  uint32_t e = S.u.lut[(inf & 0xffff) + (look >> (16 - bits))];
+  uint32_t e = T.lut[(inf & 0xffff) + (look >> (16 - bits))];
   if ((e & 31) == 0) {
-    if (e) e = S.lut2[inf >> 23][(e >> 5) - 1][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
-    if ((e & 31) == 0) e = slow_entry(S, slot, look);
+    if (e) e = T.lut2[inf >> 23][(e >> 5) - 1][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
+    if ((e & 31) == 0) e = slow_entry(T, acmask, slot, look);
   }
   return e;
 }
@@ -264,7 +280,8 @@ FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 
 // and the canonical fallback: with 64 lanes some lane starts or ends a block
 // on almost every step, so those updates are selects fed by loads issued at
 // the top of the step (next phase's table infos, next old event).
-FFCV_DEV DecState sync_range(JShared &S, const uint32_t *words, DecState st,
+template <class TB>
+FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, DecState st,
                              uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, DecState old_exit,
                              bool use_old, uint32_t &iters) {
   BitReader br;
@@ -295,7 +312,7 @@ FFCV_DEV DecState sync_range(JShared &S, const uint32_t *words, DecState st,
     const bool adv = ocur < key;
     j += adv ? 1 : 0;
     ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
-    const uint32_t e = decode_entry(S, isblk ? dinf : ainf, br.acc);
+    const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
     const int nbits = hit ? 0 : (int)(e & 31);
     br.consume(nbits);
     pos += nbits;
@@ -341,7 +358,8 @@ FFCV_DEV void locate_block(const int4 pd0, const int4 pd1, int64_t blk, int64_t 
   boff = ((uint32_t)pd0.x + (uint32_t)my * (uint32_t)pd0.y + (uint32_t)mx * (uint32_t)pd0.z) * 64u;
 }
 
-FFCV_DEV void write_range(JShared &S, const uint32_t *words, DecState st, uint32_t end_bit,
+template <class TB>
+FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecState st, uint32_t end_bit,
                           int64_t blk, int16_t *coef, int16_t *dcd, uint32_t &iters) {
   BitReader br;
   br.init(words, st.pos);
@@ -361,7 +379,7 @@ FFCV_DEV void write_range(JShared &S, const uint32_t *words, DecState st, uint32
     const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
     const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
     const bool isblk = z == 0;
-    const uint32_t e = decode_entry(S, isblk ? dinf : ainf, br.acc);
+    const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
     const int nbits = (int)(e & 31), size = (int)(e >> 5) & 15, zinc = (int)(e >> 9);
     const int raw = (int)((br.acc << (nbits - size)) >> 1 >> (63 - size));
     const int v = size ? huff_extend(raw, size) : 0;
@@ -501,6 +519,9 @@ struct JpegArgs {
   uint64_t dcd_slot;
   uint8_t *rgb;
   ImgInfo *info;
+  uint8_t *gtab;  // per-image JTables for images that cannot share the workgroup's
+  uint64_t gtab_slot;
+  int batch;
   uint32_t max_h, max_w;
   uint64_t max_blocks;
   uint64_t *dbg;
@@ -522,7 +543,7 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
   auto B = [&](uint32_t p) -> int {
     int v;
     if (p < HDR_BYTES)
-      v = S.u.hdr[p];
+      v = S.hdr[p];
     else
       v = __builtin_nontemporal_load(src + p);
     return v;
@@ -767,19 +788,194 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
   return FFCV_SAMPLE_OK;
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
-  __shared__ JShared S;
-  const int t = threadIdx.x;
-  const int k = blockIdx.x;
-  const ffcv_sample smp = a.samples[k];
-  ImgInfo *info = a.info + k;
-  if (smp.mode != 0) {  // raw samples are handled by rrc_raw_kernel / gather
-    if (t == 0) {
-      a.status[k] = FFCV_SAMPLE_OK;
-      info->status = -1;  // K2 skips
+// Wave-level syncs: K1's waves decode independent images, so after the
+// workgroup's shared table build each wave orders only its own lanes.
+FFCV_DEV void wsync_lds() {  // LDS writes of this wave visible to its lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+FFCV_DEV void wsync_mem() {  // LDS and global writes of this wave visible to its lanes
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+
+// P1: Huffman decode tables for the table slots of image R (jdhuff.c
+// jpeg_make_d_derived_tbl, including its table checks), by NT threads: the
+// workgroup into its shared LDS copy, or one wave into its own global copy.
+template <int NT, class TB, class HBF>
+FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
+  auto bar = [&]() {
+    if constexpr (NT == JT)
+      wsync_mem();
+    else
+      __syncthreads();
+  };
+  const int nslots = R.nslots;
+  if (tid == 0) T.bad = 0;
+  bar();
+  if (tid < nslots) {
+    const int tab = R.slot_tab[tid];
+    const uint32_t d = R.dht_off[tab];
+    uint32_t code = 0;
+    int kk = 0;
+    bool bad = false;
+    for (int l = 1; l <= 16; l++) {
+      int nl = HB(d + l - 1);
+      T.valoff[tid][l] = kk - (int)code;
+      code += nl;
+      kk += nl;
+      if (code >= (1u << l)) bad = true;  // over-subscribed (or all-ones) code space
+      T.lim[tid][l] = code << (16 - l);
+      code <<= 1;
     }
-    return;
+    T.nvals[tid] = kk;
+    if (bad) T.bad = 1;
+    T.nsub[tid] = 0;
+  }
+  bar();
+  for (int s2 = 0; s2 < nslots; s2++) {
+    const int tab = R.slot_tab[s2];
+    const uint32_t d = R.dht_off[tab];
+    for (int i = tid; i < T.nvals[s2]; i += NT) {
+      int v = HB(d + 16 + i);
+      if (tab < 4 && v > 15) T.bad = 1;  // DC sizes are 0..15
+      T.vals[s2][i] = (uint8_t)v;
+    }
+  }
+  if (tid == 0) T.lut[LUT_POOL - 1] = 0;  // the zero word of LUT-less slots
+  bar();
+  for (int s = 0; s < nslots; s++) {
+    const uint32_t inf = R.sinfo[s];
+    const int bits = (int)((inf >> 16) & 15);
+    if (!bits) continue;
+    const bool ac = (R.acmask >> s) & 1;
+    uint32_t L[FB_AC + 1];
+#pragma unroll
+    for (int l = 1; l <= FB_AC; l++) L[l] = T.lim[s][l];
+    for (int v = tid; v < (1 << bits); v += NT) {
+      const uint32_t look = (uint32_t)v << (16 - bits);
+      int len = 1;
+#pragma unroll
+      for (int l = 1; l < FB_AC; l++) len += (l < bits && look >= L[l]) ? 1 : 0;
+      uint32_t e = 0;
+      if (look < T.lim[s][len]) {
+        int sym = T.vals[s][(T.valoff[s][len] + (int)(look >> (16 - len))) & 0xff];
+        e = make_entry(ac, len, sym);
+      } else if (look < T.lim[s][16]) {  // codes longer than `bits` under this prefix
+        int n = atomicAdd(&T.nsub[s], 1);
+        if (n < NSUB) {
+          T.sub_prefix[s][n] = (uint16_t)v;
+          e = (uint32_t)(n + 1) << 5;
+        }
+      }
+      T.lut[(inf & 0xffff) + v] = (uint16_t)e;
+    }
+  }
+  bar();
+  for (int i = tid; i < NSLOT * NSUB * (1 << SUBB); i += NT) {
+    const int s = i / (NSUB << SUBB), n = (i >> SUBB) % NSUB, x = i & ((1 << SUBB) - 1);
+    if (s >= nslots || n >= min(T.nsub[s], NSUB)) continue;
+    const int bits = (int)((R.sinfo[s] >> 16) & 15);
+    const uint32_t look = ((uint32_t)T.sub_prefix[s][n] << (16 - bits)) | ((uint32_t)x << (16 - bits - SUBB));
+    int len = 1;
+    for (int l = 1; l < 16; l++) len += look >= T.lim[s][l];
+    T.lut2[R.sinfo[s] >> 23][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(T, R.acmask, s, look) : (uint16_t)0;
+  }
+  bar();
+}
+
+// P3-P5 with table set T (the workgroup's LDS copy or the image's global
+// copy; separate instantiations so each reads its own address space).
+template <class TB>
+FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, const uint32_t *words,
+                             uint32_t total_bits, int16_t *coef, int16_t *dcd) {
+  // ------------------------------------------------------------- P3 ----
+  STAMP(3);
+  uint32_t nthr = (total_bits + 191) / 192;
+  nthr = max(1u, min(nthr, (uint32_t)JT));
+  const uint32_t cbits = (total_bits + nthr - 1) / nthr;
+  const bool active = t < (int)nthr;
+  const uint32_t my_end = active ? (t == (int)nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
+  DecState g;
+  g.pos = active ? t * cbits : 0;
+  g.z = 0;
+  g.ph = 0;
+  uint32_t my_cnt = 0;
+  int my_nev = 0, my_cb = 0;
+  DecState e = g;
+  uint32_t it_lane = 0, it_wave = 0;  // diagnostics: loop iterations (max over lanes per round)
+  if (active) e = sync_range(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, g, false, it_lane);
+  if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
+  int rounds = 0;
+  for (;;) {
+    DecState ng;
+    ng.pos = lane_prev(e.pos);
+    ng.z = (int)lane_prev((uint32_t)e.z);
+    ng.ph = (int)lane_prev((uint32_t)e.ph);
+    const bool changed = active && t > 0 && (ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph);
+    if (!__any(changed)) break;
+    rounds++;
+    if (changed) {
+      g = ng;
+      if (g.pos >= my_end) {
+        e = g;
+        my_cnt = 0;
+        my_nev = 0;
+      } else {
+        it_lane = 0;
+        e = sync_range(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, e, true, it_lane);
+      }
+    }
+    if (a.dbg) it_wave += __reduce_max_sync(~0ull, changed ? it_lane : 0u);
+  }
+  if (!active) my_cnt = 0;
+  if (a.dbg && t == 0) {
+    a.dbg[(uint64_t)k * 16 + 12] = (uint64_t)rounds;
+    a.dbg[(uint64_t)k * 16 + 13] = (uint64_t)nthr;
+    a.dbg[(uint64_t)k * 16 + 14] = (uint64_t)it_wave;
+  }
+
+  // ------------------------------------------------------------- P4 ----
+  STAMP(4);
+  const uint32_t blk_base = wave_exscan(my_cnt);
+  bool bad_lane = false;
+  if (active) {
+    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
+    bad_lane = cur < 0 || (cur % S.bpm) != g.ph;  // inconsistent stream
+  }
+  const bool any_bad = __any(bad_lane);
+
+  // ------------------------------------------------------------- P5 ----
+  STAMP(5);
+  uint32_t it_lane2 = 0;
+  if (active && g.pos < my_end) {
+    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
+    if (cur >= 0) write_range(S, T, words, g, my_end, cur, coef, dcd, it_lane2);
+  }
+  if (a.dbg) {
+    const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
+    if (t == 0) a.dbg[(uint64_t)k * 16 + 15] = (uint64_t)wmax;
+  }
+
+  return any_bad;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(JW * JT) jpeg_entropy_kernel(JpegArgs a) {
+  __shared__ K1Shared KS;
+  const int wv = threadIdx.x / JT;  // image (wave) within the workgroup
+  const int t = threadIdx.x % JT;
+  const int k = blockIdx.x * JW + wv;
+  JShared &S = KS.w[wv];
+  const bool have = k < a.batch;
+  ffcv_sample smp = {};
+  if (have) smp = a.samples[k];
+  ImgInfo *info = a.info + k;
+  const bool live = have && smp.mode == 0;
+  if (have && smp.mode != 0 && t == 0) {  // raw samples are handled by rrc_raw_kernel / gather
+    a.status[k] = FFCV_SAMPLE_OK;
+    info->status = -1;  // K2 skips
   }
   const uint8_t *src = a.base + smp.offset;
   const uint32_t nbytes = (uint32_t)smp.size;
@@ -797,7 +993,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
 
   // ------------------------------------------------------------- P0 ----
   STAMP(0);
-  {
+  if (live) {
     // aligned dword loads (one batch per lane), bytes scattered into LDS
     const uint32_t nh = min(nbytes, (uint32_t)HDR_BYTES);
     const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
@@ -811,61 +1007,65 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int idx = b0 + j;
-        if (idx >= 0 && idx < HDR_BYTES) S.u.hdr[idx] = idx < (int)nh ? (uint8_t)(w >> (8 * j)) : 0;
+        if (idx >= 0 && idx < HDR_BYTES) S.hdr[idx] = idx < (int)nh ? (uint8_t)(w >> (8 * j)) : 0;
       }
     }
   }
+  wsync_lds();
+  if (t == 0) S.status = live ? parse_header(S, src, nbytes, smp, a, k, MODE) : -1;
   __syncthreads();
-  if (t == 0) {
-    S.status = parse_header(S, src, nbytes, smp, a, k, MODE);
-    S.any = 0;
+
+  // ------------------------------------------------------------- P1 ----
+  // The workgroup's first valid image provides the shared tables; every
+  // image whose table slots and DHT bytes equal that image's uses them.
+  STAMP(1);
+  int ref = -1;
+#pragma unroll
+  for (int w = JW - 1; w >= 0; w--)
+    if (KS.w[w].status == FFCV_SAMPLE_OK) ref = w;
+  bool match = false;
+  if (ref >= 0 && S.status == FFCV_SAMPLE_OK) {
+    const JShared &R = KS.w[ref];
+    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * JW + ref].offset;
+    match = R.nslots == S.nslots;
+    for (int q = 0; q < NSLOT; q++)
+      if (q < R.nslots && R.slot_tab[q] != S.slot_tab[q]) match = false;
+    if (match && ref != wv) {
+      bool diff = false;
+      for (int q = 0; q < R.nslots; q++) {
+        const uint32_t dr = R.dht_off[R.slot_tab[q]], ds = S.dht_off[S.slot_tab[q]];
+        auto hb = [](const JShared &X, const uint8_t *xs, uint32_t p) -> int {
+          return p < HDR_BYTES ? X.hdr[p] : __builtin_nontemporal_load(xs + p);
+        };
+        int total = 0;
+        for (int l = 0; l < 16; l++) total += hb(S, src, ds + l);
+        for (int i = t; i < 16 + total; i += JT) diff |= hb(S, src, ds + i) != hb(R, rsrc, dr + i);
+      }
+      match = !__any(diff);
+    }
   }
-  __syncthreads();
+  if (ref >= 0) {
+    const JShared &R = KS.w[ref];
+    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * JW + ref].offset;
+    auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)__builtin_nontemporal_load(rsrc + p); };
+    build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
+  }
+  // (no workgroup barrier below this point: each wave runs on its own)
+  if (!live) return;
   if (S.status != FFCV_SAMPLE_OK) {
     fail();
     return;
   }
-
-  // ------------------------------------------------------------- P1 ----
-  STAMP(1);
   auto HB = [&](uint32_t p) -> int {
     int v;
     if (p < HDR_BYTES)
-      v = S.u.hdr[p];
+      v = S.hdr[p];
     else
       v = __builtin_nontemporal_load(src + p);
     return v;
   };
-  if (t < S.nslots) {
-    // jdhuff.c jpeg_make_d_derived_tbl, including its table checks
-    const int tab = S.slot_tab[t];
-    const uint32_t d = S.dht_off[tab];
-    uint32_t code = 0;
-    int kk = 0;
-    bool bad = false;
-    for (int l = 1; l <= 16; l++) {
-      int nl = HB(d + l - 1);
-      S.valoff[t][l] = kk - (int)code;
-      code += nl;
-      kk += nl;
-      if (code >= (1u << l)) bad = true;  // over-subscribed (or all-ones) code space
-      S.lim[t][l] = code << (16 - l);
-      code <<= 1;
-    }
-    S.nvals[t] = kk;
-    if (bad) S.status = FFCV_SAMPLE_BAD_MARKER;
-    S.nsub[t] = 0;
-  }
-  __syncthreads();
-  for (int s2 = 0; s2 < S.nslots; s2++) {
-    const int tab = S.slot_tab[s2];
-    const uint32_t d = S.dht_off[tab];
-    for (int i = t; i < S.nvals[s2]; i += JT) {
-      int v = HB(d + 16 + i);
-      if (tab < 4 && v > 15) S.status = FFCV_SAMPLE_BAD_MARKER;  // DC sizes are 0..15
-      S.vals[s2][i] = (uint8_t)v;
-    }
-  }
+  JTables *gt = (JTables *)(a.gtab + a.gtab_slot * k);
+  if (!match) build_tables<JT>(*gt, S, HB, t);
   for (int i = t; i < S.ncomp * 64; i += JT) {
     int c = i >> 6, zz = i & 63;
     int tq = S.tq[c];
@@ -874,49 +1074,12 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     int n = c_natural[zz];
     info->qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
   }
-  __syncthreads();  // header bytes are dead from here (the LUT pool reuses them)
-  if (S.status != FFCV_SAMPLE_OK) {
+  wsync_lds();  // header bytes are dead from here (P2 stages into the same LDS)
+  if (match ? KS.tab.bad : gt->bad) {
+    if (t == 0) S.status = FFCV_SAMPLE_BAD_MARKER;
+    wsync_lds();
     fail();
     return;
-  }
-  const int nslots = S.nslots;
-  if (t == 0) S.u.lut[LUT_POOL - 1] = 0;  // the zero word of LUT-less slots
-  for (int s = 0; s < nslots; s++) {
-    const uint32_t inf = S.sinfo[s];
-    const int bits = (int)((inf >> 16) & 15);
-    if (!bits) continue;
-    const bool ac = (S.acmask >> s) & 1;
-    uint32_t L[FB_AC + 1];
-#pragma unroll
-    for (int l = 1; l <= FB_AC; l++) L[l] = S.lim[s][l];
-    for (int v = t; v < (1 << bits); v += JT) {
-      const uint32_t look = (uint32_t)v << (16 - bits);
-      int len = 1;
-#pragma unroll
-      for (int l = 1; l < FB_AC; l++) len += (l < bits && look >= L[l]) ? 1 : 0;
-      uint32_t e = 0;
-      if (look < S.lim[s][len]) {
-        int sym = S.vals[s][(S.valoff[s][len] + (int)(look >> (16 - len))) & 0xff];
-        e = make_entry(ac, len, sym);
-      } else if (look < S.lim[s][16]) {  // codes longer than `bits` under this prefix
-        int n = atomicAdd(&S.nsub[s], 1);
-        if (n < NSUB) {
-          S.sub_prefix[s][n] = (uint16_t)v;
-          e = (uint32_t)(n + 1) << 5;
-        }
-      }
-      S.u.lut[(inf & 0xffff) + v] = (uint16_t)e;
-    }
-  }
-  __syncthreads();
-  for (int i = t; i < NSLOT * NSUB * (1 << SUBB); i += JT) {
-    const int s = i / (NSUB << SUBB), n = (i >> SUBB) % NSUB, x = i & ((1 << SUBB) - 1);
-    if (s >= nslots || n >= min(S.nsub[s], NSUB)) continue;
-    const int bits = (int)((S.sinfo[s] >> 16) & 15);
-    const uint32_t look = ((uint32_t)S.sub_prefix[s][n] << (16 - bits)) | ((uint32_t)x << (16 - bits - SUBB));
-    int len = 1;
-    for (int l = 1; l < 16; l++) len += look >= S.lim[s][l];
-    S.lut2[S.sinfo[s] >> 23][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(S, s, look) : (uint16_t)0;
   }
   // the coefficient slot is all zeros here: the IDCT kernel zeroes every
   // block it consumes (and ffcv_jpeg_create zeroed the slot)
@@ -943,10 +1106,10 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
     // wait behind the stores (gfx9 counts loads and stores in one vmcnt).
     uint32_t fbase = 0;  // stream offset of stage[0] (a multiple of 4)
     auto flush = [&](uint32_t upto) {  // write stage bytes [fbase, upto), upto % 4 == 0
-      __syncthreads();
+      wsync_lds();
       const uint32_t nd = (upto - fbase) / 4;
       for (uint32_t q = t; q < nd; q += JT) ((uint32_t *)gds)[fbase / 4 + q] = ((const uint32_t *)S.stage)[q];
-      __syncthreads();
+      wsync_lds();
     };
     // DS_DEPTH-deep prefetch ring, unrolled so every ring register is consumed in
     // place (a rotating copy would make the compiler wait for all loads)
@@ -1014,89 +1177,23 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
         flush(upto);
         if (t < (int)(dlen - upto)) S.stage[t] = S.stage[upto - fbase + t];
         fbase = upto;
-        __syncthreads();
+        wsync_lds();
       }
     }
     // tail + zero padding (libjpeg fills zeros after a marker)
-    __syncthreads();
+    wsync_lds();
     for (uint32_t i = dlen - fbase + t; i < dlen - fbase + STREAM_PAD + 4; i += JT) S.stage[i] = 0;
     flush((dlen + STREAM_PAD + 3) & ~3u);
   }
-  __threadfence_block();
-  __syncthreads();
+  wsync_mem();
   const uint32_t *words = (const uint32_t *)gds;
   const uint32_t total_bits = dlen * 8;
 
-  // ------------------------------------------------------------- P3 ----
-  STAMP(3);
-  uint32_t nthr = (total_bits + 191) / 192;
-  nthr = max(1u, min(nthr, (uint32_t)JT));
-  const uint32_t cbits = (total_bits + nthr - 1) / nthr;
-  const bool active = t < (int)nthr;
-  const uint32_t my_end = active ? (t == (int)nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
-  DecState g;
-  g.pos = active ? t * cbits : 0;
-  g.z = 0;
-  g.ph = 0;
-  uint32_t my_cnt = 0;
-  int my_nev = 0, my_cb = 0;
-  DecState e = g;
-  uint32_t it_lane = 0, it_wave = 0;  // diagnostics: loop iterations (max over lanes per round)
-  if (active) e = sync_range(S, words, g, my_end, t, my_cnt, my_nev, my_cb, g, false, it_lane);
-  if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
-  int rounds = 0;
-  for (;;) {
-    DecState ng;
-    ng.pos = lane_prev(e.pos);
-    ng.z = (int)lane_prev((uint32_t)e.z);
-    ng.ph = (int)lane_prev((uint32_t)e.ph);
-    const bool changed = active && t > 0 && (ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph);
-    if (!__any(changed)) break;
-    rounds++;
-    if (changed) {
-      g = ng;
-      if (g.pos >= my_end) {
-        e = g;
-        my_cnt = 0;
-        my_nev = 0;
-      } else {
-        it_lane = 0;
-        e = sync_range(S, words, g, my_end, t, my_cnt, my_nev, my_cb, e, true, it_lane);
-      }
-    }
-    if (a.dbg) it_wave += __reduce_max_sync(~0ull, changed ? it_lane : 0u);
-  }
-  if (!active) my_cnt = 0;
-  if (a.dbg && t == 0) {
-    a.dbg[(uint64_t)k * 16 + 12] = (uint64_t)rounds;
-    a.dbg[(uint64_t)k * 16 + 13] = (uint64_t)nthr;
-    a.dbg[(uint64_t)k * 16 + 14] = (uint64_t)it_wave;
-  }
 
-  // ------------------------------------------------------------- P4 ----
-  STAMP(4);
-  const uint32_t blk_base = wave_exscan(my_cnt);
-  bool bad_lane = false;
-  if (active) {
-    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    bad_lane = cur < 0 || (cur % S.bpm) != g.ph;  // inconsistent stream
-  }
-  const bool any_bad = __any(bad_lane);
-
-  // ------------------------------------------------------------- P5 ----
-  STAMP(5);
   int16_t *dcd = a.dcd + a.dcd_slot * k;
-  uint32_t it_lane2 = 0;
-  if (active && g.pos < my_end) {
-    int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur >= 0) write_range(S, words, g, my_end, cur, coef, dcd, it_lane2);
-  }
-  if (a.dbg) {
-    const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
-    if (t == 0) a.dbg[(uint64_t)k * 16 + 15] = (uint64_t)wmax;
-  }
-  __threadfence_block();
-  __syncthreads();
+  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, words, total_bits, coef, dcd)
+                             : entropy_passes(S, *gt, a, k, t, words, total_bits, coef, dcd);
+  wsync_mem();
 
   // ------------------------------------------------------------- P6 ----
   // DC prediction (jdhuff.c last_dc_val): per-component running sum of DC
@@ -1139,8 +1236,7 @@ __global__ void __launch_bounds__(JT) jpeg_entropy_kernel(JpegArgs a) {
       }
     }
   }
-  __threadfence_block();
-  __syncthreads();
+  wsync_mem();
 
   if (MODE == JM_COEF) {
     int16_t *o = (int16_t *)a.out + a.out_stride / 2 * k;
@@ -1661,6 +1757,8 @@ struct ffcv_jpeg_ctx {
   uint64_t dcd_slot;
   uint8_t *rgb;  // K2 band staging when a band's source rows exceed LDS
   ImgInfo *info;
+  uint8_t *gtab;
+  uint64_t gtab_slot;
   uint64_t nblk;
 };
 
@@ -1673,6 +1771,7 @@ static void free_ctx(ffcv_jpeg_ctx *c) {
   (void)hipFree(c->dcd);
   (void)hipFree(c->rgb);
   (void)hipFree(c->info);
+  (void)hipFree(c->gtab);
   delete c;
 }
 
@@ -1697,6 +1796,7 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
   c->plane_slot = align_up(nblk * 64, 256);  // bytes
   c->dcd_slot = align_up(nblk, 128);         // int16 elements
   c->nblk = nblk;
+  c->gtab_slot = align_up(sizeof(JTables), 256);
   hipError_t e;
   if ((e = hipMalloc(&c->dstuff, c->dstuff_slot * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->coef, c->coef_slot * 2 * max_batch)) != hipSuccess ||
@@ -1704,6 +1804,7 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
       (e = hipMalloc(&c->dcd, c->dcd_slot * 2 * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->rgb, c->plane_slot * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
+      (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess ||
       // the entropy kernel writes only non-zero coefficients into an
       // all-zero slot; the IDCT kernel restores the zeros it consumed
       (e = hipMemset(c->coef, 0, c->coef_slot * 2 * max_batch)) != hipSuccess ||
@@ -1731,8 +1832,10 @@ int ffcv_jpeg_destroy(ffcv_jpeg_ctx *c) {
   return FFCV_OK;
 }
 
-static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_sample *samples, int32_t *status) {
+static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_sample *samples, int batch,
+                          int32_t *status) {
   JpegArgs a = {};
+  a.batch = batch;
   a.base = base;
   a.samples = samples;
   a.status = status;
@@ -1746,6 +1849,8 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.dcd_slot = c->dcd_slot;
   a.rgb = c->rgb;
   a.info = c->info;
+  a.gtab = c->gtab;
+  a.gtab_slot = c->gtab_slot;
   a.max_h = c->max_h;
   a.max_w = c->max_w;
   a.dbg = c->dbg;
@@ -1777,7 +1882,7 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
     return FFCV_EINVAL;
   }
   if (batch == 0) return FFCV_OK;
-  JpegArgs a = make_args(c, base, samples, status);
+  JpegArgs a = make_args(c, base, samples, batch, status);
   a.crops = crops;
   a.cut = cutout_yx;
   a.flips = flips;
@@ -1787,12 +1892,21 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
   a.out_stride = p->out_stride ? p->out_stride : dense;
   hipStream_t s = ffcv::as_stream(stream);
-  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3(batch), dim3(JT), 0, s, a);
-  FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
-  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
-  FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
+  // diagnostics only (timing of one kernel re-run on the previous batch's
+  // scratch): FFCV_JPEG_ONLY bit 0 = K1, bit 1 = K1b, bit 2 = K2
+  const char *only_s = getenv("FFCV_JPEG_ONLY");
+  const int only = only_s ? atoi(only_s) : 7;
+  if (only & 1) {
+    hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0, s, a);
+    FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
+  }
+  if (only & 2) {
+    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
+    FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
+  }
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
-  if (fp16)
+  if (!(only & 4)) {
+  } else if (fp16)
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, true>), g2, dim3(K2T), K2_LDS, s, a);
   else
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, false>), g2, dim3(K2T), K2_LDS, s, a);
@@ -1809,11 +1923,11 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
     return FFCV_EINVAL;
   }
   if (batch == 0) return FFCV_OK;
-  JpegArgs a = make_args(c, base, samples, status);
+  JpegArgs a = make_args(c, base, samples, batch, status);
   a.out = out;
   a.out_stride = out_stride;
   hipStream_t s = ffcv::as_stream(stream);
-  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3(batch), dim3(JT), 0, s, a);
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
@@ -1829,11 +1943,12 @@ int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *
   int rc = check_common("ffcv_jpeg_coefficients_batch", c, base, samples, batch, coefs, status);
   if (rc) return rc;
   if (batch == 0) return FFCV_OK;
-  JpegArgs a = make_args(c, base, samples, status);
+  JpegArgs a = make_args(c, base, samples, batch, status);
   a.out = coefs;
   a.out_stride = max_blocks * 64 * 2;
   a.max_blocks = max_blocks;
-  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3(batch), dim3(JT), 0, ffcv::as_stream(stream), a);
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0,
+                     ffcv::as_stream(stream), a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<COEF>");
   return FFCV_OK;
 }

@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libffcv_hip.so')
+# FFCV_HIP_LIB: diagnostic A/B of an alternative build of the same sources
+LIB_PATH = os.environ.get('FFCV_HIP_LIB') or os.path.join(_HERE, 'libffcv_hip.so')
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int

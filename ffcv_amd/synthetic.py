@@ -30,11 +30,12 @@ def natural_image(rng, h, w):
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
-def encode_jpeg(img, quality=90, subsampling='4:2:0'):
+def encode_jpeg(img, quality=90, subsampling='4:2:0', optimize=False):
     from PIL import Image
     b = io.BytesIO()
     mode = 'L' if img.ndim == 2 else 'RGB'
-    Image.fromarray(img, mode).save(b, format='JPEG', quality=quality, subsampling=subsampling)
+    Image.fromarray(img, mode).save(b, format='JPEG', quality=quality, subsampling=subsampling,
+                                    optimize=optimize)
     return np.frombuffer(b.getvalue(), np.uint8).copy()
 
 

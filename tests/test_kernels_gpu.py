@@ -193,7 +193,9 @@ def _jpeg_set(rng, n, max_side=256):
         if k % 17 == 16:
             img = img[:, :, 0].copy()
         q = [90, 95, 75, 50, 100][k % 5]
-        blobs.append(encode_jpeg(img, q, subs[k % 3]))
+        # per-image optimised Huffman tables in some samples: their workgroup
+        # cannot share one table set (K1's per-image global-table path)
+        blobs.append(encode_jpeg(img, q, subs[k % 3], optimize=k % 7 == 3))
         imgs.append(img)
     return imgs, blobs
 

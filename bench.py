@@ -140,7 +140,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)
     ap.add_argument('--only', type=int, default=0,
-                    help='diagnostic: timed steps launch only these decode kernels (bit 0 K1, 1 K1b, 2 K2)')
+                    help='diagnostic: timed steps launch only these decode kernels (bit 0 K1, bit 2 K2)')
     ap.add_argument('--inflight', type=int, default=16,
                     help='batches in flight on separate HIP streams (Loader batches_ahead analogue)')
     args = ap.parse_args()
@@ -320,7 +320,7 @@ def main():
                    'parallelism': f'dp{world} (traversal-order sharding, no collectives)'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': None,
-                     'kernel': ('jpeg_entropy_kernel<RRC> + jpeg_idct_kernel + jpeg_color_resize_kernel<RRC,fp16> '
+                     'kernel': ('jpeg_entropy_kernel<RRC> + jpeg_color_resize_kernel<RRC,fp16> '
                                 '(one decode launch sequence, HIP events on the slot stream)'
                                 if mode == 'jpg' else 'rrc_raw_kernel'),
                      'kernel_ms': round(kern_ms, 4), 'algorithmic_bytes_per_image': round(unit_bytes, 1),
@@ -332,7 +332,7 @@ def main():
     prof = os.path.join(ROOT, 'profiles', f'traffic_{args.config}.json')
     if os.path.exists(prof):
         pm = json.load(open(prof))
-        names = (['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', 'jpeg_color_resize_kernel<0, true>']
+        names = (['jpeg_entropy_kernel<0>', 'jpeg_color_resize_kernel<0, true>']
                  if mode == 'jpg' else ['rrc_raw_kernel<false>'])
         if all(n in pm and 'fetch_size_kb' in pm[n] and 'write_size_kb' in pm[n] for n in names):
             tb = sum((pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 for n in names)

@@ -89,7 +89,6 @@ struct ImgInfo {
   // component, and the ifast multipliers
   int32_t wx0[3], wy0[3], wbw[3], wbh[3], bw[3];
   uint64_t coff[3];
-  int16_t qmul[3][64];
 };
 
 // Huffman decode tables built from one image's DHT segments.  K1 runs JW
@@ -143,6 +142,7 @@ struct JShared {
   // in its component's plane, blocks per MCU row step, hs, and the window
   // as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
   int4 pdesc[10][2];
+  int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
   union {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
     uint32_t ev[2][NEV + 1][JT];  // P3: block-start events (pos << 4 | phase), double-buffered
@@ -497,6 +497,28 @@ FFCV_DEV void idct_ifast_block(int d[64], uint8_t *out, int stride) {
     v.y = o4 | (o5 << 8) | (o6 << 16) | (o7 << 24);
     *(uint2 *)(out + (uint64_t)r * stride) = v;
   }
+}
+
+// One block: load the zigzag coefficients at cp and zero them, de-zigzag +
+// jidctfst.c DEQUANTIZE (int16 x int16 -> int) with the multipliers qm, and
+// the ifast IDCT into out (stride bytes per row).
+FFCV_DEV void idct_block(int16_t *cp, const int16_t *qm, uint8_t *out, int stride) {
+  int16_t zz[64];
+  int d[64];
+#pragma unroll
+  for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
+#pragma unroll
+  for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
+  int mag = 0;
+#pragma unroll
+  for (int n = 0; n < 64; n++) {
+    d[n] = (int)zz[kZigzagOfNatural[n]] * (int)qm[n];
+    mag |= d[n] < 0 ? -d[n] : d[n];
+  }
+  if (mag < (1 << 14))
+    idct_ifast_block<false>(d, out, stride);
+  else
+    idct_ifast_block<true>(d, out, stride);
 }
 
 struct JpegArgs {
@@ -962,7 +984,13 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(JW * JT) jpeg_entropy_kernel(JpegArgs a) {
+// Waves per SIMD K1 is compiled for: 4 (= the LDS limit, 16 images per CU)
+// caps it at 128 VGPRs and spills a few; 3 measured equal or slightly faster
+// in the full pipeline (K2's workgroups share the CUs).
+#ifndef K1_WPE
+#define K1_WPE 3
+#endif
+__global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1_WPE))) jpeg_entropy_kernel(JpegArgs a) {
   __shared__ K1Shared KS;
   const int wv = threadIdx.x / JT;  // image (wave) within the workgroup
   const int t = threadIdx.x % JT;
@@ -1072,7 +1100,7 @@ __global__ void __launch_bounds__(JW * JT) jpeg_entropy_kernel(JpegArgs a) {
     uint32_t q = S.dqt_off[tq];
     int qv = S.dqt_prec[tq] ? ((HB(q + 2 * zz) << 8) | HB(q + 2 * zz + 1)) : HB(q + zz);
     int n = c_natural[zz];
-    info->qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
+    S.qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
   }
   wsync_lds();  // header bytes are dead from here (P2 stages into the same LDS)
   if (match ? KS.tab.bad : gt->bad) {
@@ -1263,7 +1291,7 @@ __global__ void __launch_bounds__(JW * JT) jpeg_entropy_kernel(JpegArgs a) {
   }
 
   // ------------------------------------------------------------- P7 ----
-  // geometry + window + multipliers for jpeg_idct_kernel and K2
+  // geometry + crop window for K2
   STAMP(7);
   if (t == 0) {
     info->status = FFCV_SAMPLE_OK;
@@ -1292,55 +1320,36 @@ __global__ void __launch_bounds__(JW * JT) jpeg_entropy_kernel(JpegArgs a) {
     info->rw = S.rw;
     a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
   }
-  STAMP(8);
-}
 
-// ======================================================================= //
-// K1b: de-zigzag + dequantise + ifast IDCT of every window block, one      //
-// thread per block over the whole batch; each block is zeroed after it is  //
-// read, which keeps the coefficient slot all-zero for the next batch.      //
-// ======================================================================= //
-#define IDCT_T 256
-__global__ void __launch_bounds__(IDCT_T) jpeg_idct_kernel(JpegArgs a) {
-  const int k = blockIdx.y;
-  const ImgInfo *I = a.info + k;
-  if (I->status != FFCV_SAMPLE_OK) return;
-  int i = blockIdx.x * IDCT_T + threadIdx.x;
-  const int n0 = I->wbw[0] * I->wbh[0], n1 = I->wbw[1] * I->wbh[1], n2 = I->wbw[2] * I->wbh[2];
-  if (i >= n0 + n1 + n2) return;
-  int c = 0;
-  if (i >= n0) {
-    i -= n0;
-    c = 1;
-    if (i >= n1) {
-      i -= n1;
-      c = 2;
+  // ------------------------------------------------------------- P8 ----
+  // de-zigzag + dequantise + ifast IDCT (jidctfst.c) of the window's blocks,
+  // one block per lane; each block is zeroed after it is read, which keeps
+  // the coefficient slot all-zero for the next batch.
+  STAMP(8);
+  {
+    uint8_t *planes = a.planes + a.plane_slot * k;
+    int nb[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) nb[c] = c < S.ncomp ? (S.wx1[c] - S.wx0[c] + 1) * (S.wy1[c] - S.wy0[c] + 1) : 0;
+    const int ntot = nb[0] + nb[1] + nb[2];
+    for (int i = t; i < ntot; i += JT) {
+      int c = 0, j = i;
+      if (j >= nb[0]) {
+        j -= nb[0];
+        c = 1;
+        if (j >= nb[1]) {
+          j -= nb[1];
+          c = 2;
+        }
+      }
+      const int wbw = S.wx1[c] - S.wx0[c] + 1;
+      const int by = S.wy0[c] + j / wbw, bx = S.wx0[c] + j % wbw;
+      const int stride = S.bw[c] * 8;
+      idct_block(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64, S.qmul[c],
+                 planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
     }
   }
-  const int wbw = I->wbw[c];
-  const int by = I->wy0[c] + i / wbw, bx = I->wx0[c] + i % wbw;
-  int16_t *cp = a.coef + a.coef_slot * k + (I->coff[c] + (uint64_t)by * I->bw[c] + bx) * 64;
-  int16_t zz[64], q[64];
-  int d[64];
-#pragma unroll
-  for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
-#pragma unroll
-  for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(q + p8 * 8) = ((const uint4 *)I->qmul[c])[p8];
-#pragma unroll
-  for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
-  // de-zigzag + jidctfst.c DEQUANTIZE (int16 x int16 -> int)
-  int mag = 0;
-#pragma unroll
-  for (int n = 0; n < 64; n++) {
-    d[n] = (int)zz[kZigzagOfNatural[n]] * (int)q[n];
-    mag |= d[n] < 0 ? -d[n] : d[n];
-  }
-  const int stride = I->stride[c];
-  uint8_t *out = a.planes + a.plane_slot * k + I->poff[c] + (uint64_t)by * 8 * stride + bx * 8;
-  if (mag < (1 << 14))
-    idct_ifast_block<false>(d, out, stride);
-  else
-    idct_ifast_block<true>(d, out, stride);
+  STAMP(9);
 }
 
 // ======================================================================= //
@@ -1893,16 +1902,12 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   a.out_stride = p->out_stride ? p->out_stride : dense;
   hipStream_t s = ffcv::as_stream(stream);
   // diagnostics only (timing of one kernel re-run on the previous batch's
-  // scratch): FFCV_JPEG_ONLY bit 0 = K1, bit 1 = K1b, bit 2 = K2
+  // scratch): FFCV_JPEG_ONLY bit 0 = K1, bit 2 = K2
   const char *only_s = getenv("FFCV_JPEG_ONLY");
   const int only = only_s ? atoi(only_s) : 7;
   if (only & 1) {
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0, s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
-  }
-  if (only & 2) {
-    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
-    FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
   }
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (!(only & 4)) {
@@ -1929,8 +1934,6 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   hipStream_t s = ffcv::as_stream(stream);
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
-  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((c->nblk + IDCT_T - 1) / IDCT_T), batch), dim3(IDCT_T), 0, s, a);
-  FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
   dim3 g2((c->max_h + BAND - 1) / BAND, batch);
   hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_FULL, false>), g2, dim3(K2T), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<FULL>");

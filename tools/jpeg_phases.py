@@ -38,14 +38,14 @@ for it in range(3):
     dec.rrc(d_data, d_smp, B, crops, cut, None, rp, out, status)
     torch.cuda.synchronize(); print('iter', it, 'ms', (time.perf_counter() - t0) * 1e3)
 d = dbg.cpu().numpy()
-names = ['parse', 'tables+zero', 'destuff', 'sync', 'scan', 'write', 'dcpred', 'idct']
+names = ['parse', 'tables', 'destuff', 'sync', 'scan', 'write', 'dcpred', 'info', 'idct']
 print('phase means (us):')
 for i, n in enumerate(names):
     dt = (d[:, i + 1] - d[:, i]) / 100.0
     print(f'  {n:12s} mean {dt.mean():8.1f}  p50 {np.median(dt):8.1f}  max {dt.max():8.1f}')
-tot = (d[:, 8] - d[:, 0]) / 100.0
+tot = (d[:, 9] - d[:, 0]) / 100.0
 print('  total        mean', tot.mean(), 'max', tot.max())
-print('span of K1 us', (d[:, 8].max() - d[:, 0].min()) / 100.0)
+print('span of K1 us', (d[:, 9].max() - d[:, 0].min()) / 100.0)
 print('rounds hist', np.bincount(d[:, 12].astype(int))[:20], 'nthr mean', d[:, 13].mean())
 st = (d[:, 0] - d[:, 0].min()) / 100.0
 print('start offsets us: p50', np.median(st), 'max', st.max())

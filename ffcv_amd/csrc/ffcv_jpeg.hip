@@ -70,7 +70,9 @@
 #define STREAM_PAD 32   // zero bytes after the de-stuffed stream
 #define BAND 16
 #define K2T 256
-#define K2_LDS 49152
+#ifndef K2_LDS
+#define K2_LDS 32768
+#endif
 #ifndef JW
 #define JW 4  // images (waves) per K1 workgroup
 #endif
@@ -549,7 +551,8 @@ struct JpegArgs {
   uint64_t *dbg;
   int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs;
                 // timing only (wrong output): bit 3 skips the colour pass, bit 4 the resize arithmetic;
-                // bit 5 disables the separable linear resize, bit 6 the 4:2:0 quad colour pass
+                // bit 5 disables the separable linear resize, bit 6 the 4:2:0 quad colour pass,
+                // bit 7 the linear fast path
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1527,6 +1530,169 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   band_rows(P, oy0, oy1, &r0, &r1);
   const int nrows = r1 - r0 + 1;
   const int step = rw * 3;
+  // Epilogue parameters (flip, cutout) of this image
+  Epilogue ep;
+  ep.out_h = out_h;
+  ep.out_w = out_w;
+  ep.cut_size = a.cut ? a.p.cutout_size : 0;
+  ep.cut_y = a.cut ? a.cut[2 * k] : 0;
+  ep.cut_x = a.cut ? a.cut[2 * k + 1] : 0;
+  ep.flip = a.flips ? a.flips[k] : 0;
+  ep.cut_before_flip = a.p.cutout_fill[3];
+  ep.fill[0] = a.p.cutout_fill[0];
+  ep.fill[1] = a.p.cutout_fill[1];
+  ep.fill[2] = a.p.cutout_fill[2];
+
+  // ---- linear fast path (kind 3 with the SSE2 vertical body on every
+  // element: every RRC crop that is upscaled along some axis at out_w 224).
+  // LDS: [LUT][row taps][component tiles, dword rows][crop rows as RGBx
+  // words].  Each thread owns one output column pair and walks its half of
+  // the band's rows, keeping the two source rows' horizontal sums in
+  // registers (resize.cpp HResizeLinear -> VResizeLinearVec_32s8u).
+  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= K2T && !(a.k2flags & 128)) {
+    const int lut_b = FP16 ? 1536 : 0;
+    LinTap *rtab = (LinTap *)(lds + lut_b);
+    int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
+    int need = lut_b + (int)sizeof(LinTap) * BAND;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      if (c >= ncomp) {
+        ty0[c] = tx0[c] = trows[c] = tpitch[c] = toff[c] = 0;
+        continue;
+      }
+      const int he = G.he[c], ve = G.ve[c];
+      int y0 = (ri + r0) / ve - (ve == 2 ? 1 : 0), y1 = (ri + r1) / ve + (ve == 2 ? 1 : 0);
+      int x0 = rj / he - (he == 2 ? 1 : 0), x1 = (rj + rw - 1) / he + (he == 2 ? 1 : 0);
+      y0 = max(y0, 0);
+      x0 = max(x0, 0);
+      y1 = min(y1, G.ch[c] - 1);
+      x1 = min(x1, G.cw[c] - 1);
+      ty0[c] = y0;
+      tx0[c] = x0 & ~3;  // whole dwords of the plane row (rows are 8-byte aligned)
+      trows[c] = y1 - y0 + 1;
+      tpitch[c] = ((x1 + 4) & ~3) - tx0[c];
+      toff[c] = need;
+      need += trows[c] * tpitch[c];
+    }
+    const int rgb_off = need;
+    need += nrows * rw * 4;
+    if (need <= K2_LDS) {
+      uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
+      if (t < oy1 - oy0) rtab[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+      TPlane tp[3];
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        uint32_t *tl = (uint32_t *)(lds + toff[c]);
+        const int wpr = tpitch[c] >> 2, n = trows[c] * wpr;
+        const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
+        for (int i = t; i < n; i += K2T) {
+          const int rr = i / wpr, q = i - rr * wpr;
+          tl[i] = *(const uint32_t *)(src + (uint64_t)rr * gp[c].stride + 4 * q);
+        }
+        tp[c] = TPlane{(const uint8_t *)tl, ty0[c], tx0[c], tpitch[c]};
+      }
+      __syncthreads();
+      const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
+      if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
+          G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {
+        // 4:2:0: one thread per chroma sample, its 2x2 pixel quad
+        const int R0 = Y0 >> 1, C0 = X0 >> 1, qcols = (X1 >> 1) - C0 + 1;
+        const int nq = ((Y1 >> 1) - R0 + 1) * qcols;
+        for (int i = t; i < nq; i += K2T) {
+          const int qr = i / qcols, R = R0 + qr, C = C0 + (i - qr * qcols);
+          int cb[4], cr[4];
+          upsample_quad_h2v2(tp[1], G.cw[1], G.ch[1], R, C, cb);
+          upsample_quad_h2v2(tp[2], G.cw[2], G.ch[2], R, C, cr);
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const int Y = 2 * R + (u >> 1), X = 2 * C + (u & 1);
+            if (Y < Y0 || Y > Y1 || X < X0 || X > X1) continue;
+            int v[3];
+            ycc_rgb(tp[0].at(Y, X), cb[u], cr[u], v);
+            rgbx[(Y - Y0) * rw + (X - X0)] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
+          }
+        }
+      } else {
+        for (int i = t; i < nrows * rw; i += K2T) {
+          const int yy = i / rw, x = i - yy * rw;
+          int v[3];
+          pixel_rgb(G, tp, Y0 + yy, X0 + x, v);
+          rgbx[i] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
+        }
+      }
+      __syncthreads();
+      const int tx = t % (K2T / 2), sub = t / (K2T / 2);
+      if (tx >= out_w / 2) return;
+      const int dx0 = 2 * tx;
+      const LinTap l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
+      const LinTap l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
+      // horizontal pass of crop row r for both columns: sat_s16(h >> 4) per channel
+      auto hrow = [&](int r, int H[6]) {
+        const uint32_t *row = rgbx + (r - r0) * rw;
+        const uint32_t p0 = row[l0.s], q0 = row[l0.border ? l0.s : l0.s + 1];
+        const uint32_t p1 = row[l1.s], q1 = row[l1.border ? l1.s : l1.s + 1];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+          const int a0 = (p0 >> (8 * c)) & 255, b0 = (q0 >> (8 * c)) & 255;
+          const int a1 = (p1 >> (8 * c)) & 255, b1 = (q1 >> (8 * c)) & 255;
+          H[c] = sat_s16i((l0.border ? a0 * 2048 : a0 * l0.c0 + b0 * l0.c1) >> 4);
+          H[3 + c] = sat_s16i((l1.border ? a1 * 2048 : a1 * l1.c0 + b1 * l1.c1) >> 4);
+        }
+      };
+      const int half = (BAND + 1) / 2;
+      const int ya = oy0 + sub * half, yb = min(oy1, ya + half);
+      int ca = -1, cb = -1;
+      int HA[6], HB[6];
+      for (int dy = ya; dy < yb; dy++) {
+        const LinTap ly = rtab[dy - oy0];
+        const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
+        if (ra != ca) {
+          if (ra == cb) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) HA[i] = HB[i];
+          } else {
+            hrow(ra, HA);
+          }
+          ca = ra;
+        }
+        if (rb != cb) {
+          hrow(rb, HB);
+          cb = rb;
+        }
+        int o[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+          const int m0 = (HA[i] * ly.c0) >> 16, m1 = (HB[i] * ly.c1) >> 16;
+          o[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
+        }
+        if (ep.in_cut(dy, dx0)) {
+          o[0] = ep.fill[0];
+          o[1] = ep.fill[1];
+          o[2] = ep.fill[2];
+        }
+        if (ep.in_cut(dy, dx0 + 1)) {
+          o[3] = ep.fill[0];
+          o[4] = ep.fill[1];
+          o[5] = ep.fill[2];
+        }
+        const uint64_t p0 = (uint64_t)dy * out_w + dx0;
+        if (FP16) {
+          uint32_t *o32 = (uint32_t *)((uint16_t *)ob + p0 * 3);  // 12-byte group, 4-byte aligned
+          const uint32_t h0 = s_lut[o[0] * 3], h1 = s_lut[o[1] * 3 + 1], h2 = s_lut[o[2] * 3 + 2];
+          const uint32_t h3 = s_lut[o[3] * 3], h4 = s_lut[o[4] * 3 + 1], h5 = s_lut[o[5] * 3 + 2];
+          o32[0] = h0 | (h1 << 16);
+          o32[1] = h2 | (h3 << 16);
+          o32[2] = h4 | (h5 << 16);
+        } else {
+          uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);
+          o16[0] = (uint16_t)(o[0] | (o[1] << 8));
+          o16[1] = (uint16_t)(o[2] | (o[3] << 8));
+          o16[2] = (uint16_t)(o[4] | (o[5] << 8));
+        }
+      }
+      return;
+    }
+  }
   // LDS: [LUT][column + row taps][component tiles][RGB rows].  The taps of
   // the band's rows and of every output column are computed once per
   // workgroup; the tiles cover every plane sample the band's upsampling
@@ -1661,17 +1827,6 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
     }
     __syncthreads();
   }
-  Epilogue ep;
-  ep.out_h = out_h;
-  ep.out_w = out_w;
-  ep.cut_size = a.cut ? a.p.cutout_size : 0;
-  ep.cut_y = a.cut ? a.cut[2 * k] : 0;
-  ep.cut_x = a.cut ? a.cut[2 * k + 1] : 0;
-  ep.flip = a.flips ? a.flips[k] : 0;
-  ep.cut_before_flip = a.p.cutout_fill[3];
-  ep.fill[0] = a.p.cutout_fill[0];
-  ep.fill[1] = a.p.cutout_fill[1];
-  ep.fill[2] = a.p.cutout_fill[2];
   LdsRoi lr{roi, r0, step};
   RoiSrc gr{groi, (uint64_t)step};
   auto px = [&](int dy, int dx, int v[3]) {

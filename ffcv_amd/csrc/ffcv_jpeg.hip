@@ -53,7 +53,14 @@
 #include "api_internal.h"
 #include "device_common.h"
 
-#define JT 64           // lanes per image (one wave)
+#define JT 64           // lanes per wave
+// JL = 32 (two images per wave, each with twice the bits per lane) is
+// supported and bit-exact, but measured 35% slower than 64 in round 1: the
+// longer per-image latency outweighed the ~25% fewer sync lane-steps.
+#ifndef JL
+#define JL 64           // lanes per image: a wave decodes JT / JL images side by side
+#endif
+#define IPW (JT / JL)   // images per wave
 #define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
 #define LUT_POOL 5121   // first-level LUT words shared by the slots (+ the zero word)
 #define FB_AC 11        // first-level bits, AC tables
@@ -66,7 +73,7 @@
 #define NEV 8
 #define DS_FLUSH 16     // de-stuff steps per LDS -> HBM flush
 #define DS_DEPTH 8      // de-stuff loads in flight per lane
-#define STAGE_DUMMY (2 * (NEV + 1) * JT * 4 - 4)
+#define STAGE_DUMMY (2 * (NEV + 1) * JL * 4 - 4)
 #define STREAM_PAD 32   // zero bytes after the de-stuffed stream
 #define BAND 16
 #define K2T 256
@@ -74,7 +81,7 @@
 #define K2_LDS 32768
 #endif
 #ifndef JW
-#define JW 4  // images (waves) per K1 workgroup
+#define JW 4  // waves per K1 workgroup
 #endif
 
 enum JMode { JM_RRC = 0, JM_FULL = 1, JM_COEF = 2 };
@@ -147,14 +154,14 @@ struct JShared {
   int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
   union {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
-    uint32_t ev[2][NEV + 1][JT];  // P3: block-start events (pos << 4 | phase), double-buffered
-    uint8_t stage[2 * (NEV + 1) * JT * 4];  // P2: de-stuffed bytes awaiting a flush
+    uint32_t ev[2][NEV + 1][JL];  // P3: block-start events (pos << 4 | phase), double-buffered
+    uint8_t stage[2 * (NEV + 1) * JL * 4];  // P2: de-stuffed bytes awaiting a flush
   };
 };
 
 struct K1Shared {
   JTables tab;
-  JShared w[JW];
+  JShared w[JW * IPW];
 };
 
 // zigzag index of each natural (row-major) coefficient position; the entropy
@@ -304,12 +311,12 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
     iters++;
     const int nph = ph + 1 == bpm ? 0 : ph + 1;
     const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
-    const uint32_t onext = evo[min(j + 1, NEV) * JT];
+    const uint32_t onext = evo[min(j + 1, NEV) * JL];
     const bool isblk = z == 0;
     const uint32_t key = (pos << 4) | (uint32_t)ph;
     hit = isblk && ocur == key;
     const bool rec = isblk && !hit;
-    evn[(rec ? min(n, NEV) : NEV) * JT] = key;
+    evn[(rec ? min(n, NEV) : NEV) * JL] = key;
     n += rec ? 1 : 0;
     const bool adv = ocur < key;
     j += adv ? 1 : 0;
@@ -329,7 +336,7 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
     int m = n;
     if (n < NEV) {
       int keep = min(onev - j, NEV - n);
-      for (int q = 0; q < keep; q++) evn[(n + q) * JT] = evo[(j + q) * JT];
+      for (int q = 0; q < keep; q++) evn[(n + q) * JL] = evo[(j + q) * JL];
       m = n + keep;
     }
     nev = min(m, NEV);
@@ -428,6 +435,40 @@ FFCV_DEV uint32_t lane_prev(uint32_t v) { return (uint32_t)__builtin_amdgcn_upda
 FFCV_DEV uint32_t lane_next(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false); }
 FFCV_DEV uint32_t lane_read(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
 FFCV_DEV int32_t wave_exscan_i(int32_t v) { return (int32_t)wave_exscan((uint32_t)v); }
+
+// The same over the JL-lane segments of a wave (one image each); t = lane in
+// the segment, sg = segment.  Cross-segment DPP sources are masked off.
+FFCV_DEV uint32_t seg_exscan(uint32_t v) {
+  if constexpr (JL == JT) return wave_exscan(v);
+  int x = (int)v;  // row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 into rows 1 and 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  return (uint32_t)x - v;
+}
+FFCV_DEV int32_t seg_exscan_i(int32_t v) { return (int32_t)seg_exscan((uint32_t)v); }
+FFCV_DEV uint32_t seg_prev(uint32_t v, int t) {
+  const uint32_t p = lane_prev(v);
+  return t == 0 ? 0u : p;
+}
+FFCV_DEV uint32_t seg_next(uint32_t v, int t) {
+  const uint32_t n = lane_next(v);
+  return t == JL - 1 ? 0u : n;
+}
+// value of lane i of this lane's segment (i uniform)
+FFCV_DEV uint32_t seg_read(uint32_t v, int i, int sg) {
+  if constexpr (JL == JT) return lane_read(v, i);
+  const uint32_t a = lane_read(v, i), b = lane_read(v, JL + i);
+  return sg ? b : a;
+}
+FFCV_DEV uint64_t seg_ballot(bool p, int sg) {
+  const uint64_t m = __ballot(p);
+  if constexpr (JL == JT) return m;
+  return (m >> (JL * sg)) & ((1ull << JL) - 1);
+}
+FFCV_DEV bool seg_any(bool p, int sg) { return seg_ballot(p, sg) != 0; }
 
 
 // libjpeg post-IDCT range limit: table[x & 1023] (jdmaster.c)
@@ -831,7 +872,7 @@ FFCV_DEV void wsync_mem() {  // LDS and global writes of this wave visible to it
 template <int NT, class TB, class HBF>
 FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
   auto bar = [&]() {
-    if constexpr (NT == JT)
+    if constexpr (NT == JL)
       wsync_mem();
     else
       __syncthreads();
@@ -913,12 +954,12 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
 // P3-P5 with table set T (the workgroup's LDS copy or the image's global
 // copy; separate instantiations so each reads its own address space).
 template <class TB>
-FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, const uint32_t *words,
+FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, int sg, const uint32_t *words,
                              uint32_t total_bits, int16_t *coef, int16_t *dcd) {
   // ------------------------------------------------------------- P3 ----
   STAMP(3);
   uint32_t nthr = (total_bits + 191) / 192;
-  nthr = max(1u, min(nthr, (uint32_t)JT));
+  nthr = max(1u, min(nthr, (uint32_t)JL));
   const uint32_t cbits = (total_bits + nthr - 1) / nthr;
   const bool active = t < (int)nthr;
   const uint32_t my_end = active ? (t == (int)nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
@@ -935,9 +976,9 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   int rounds = 0;
   for (;;) {
     DecState ng;
-    ng.pos = lane_prev(e.pos);
-    ng.z = (int)lane_prev((uint32_t)e.z);
-    ng.ph = (int)lane_prev((uint32_t)e.ph);
+    ng.pos = seg_prev(e.pos, t);
+    ng.z = (int)seg_prev((uint32_t)e.z, t);
+    ng.ph = (int)seg_prev((uint32_t)e.ph, t);
     const bool changed = active && t > 0 && (ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph);
     if (!__any(changed)) break;
     rounds++;
@@ -963,13 +1004,13 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 
   // ------------------------------------------------------------- P4 ----
   STAMP(4);
-  const uint32_t blk_base = wave_exscan(my_cnt);
+  const uint32_t blk_base = seg_exscan(my_cnt);
   bool bad_lane = false;
   if (active) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
     bad_lane = cur < 0 || (cur % S.bpm) != g.ph;  // inconsistent stream
   }
-  const bool any_bad = __any(bad_lane);
+  const bool any_bad = seg_any(bad_lane, sg);
 
   // ------------------------------------------------------------- P5 ----
   STAMP(5);
@@ -995,10 +1036,11 @@ template <int MODE>
 #endif
 __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1_WPE))) jpeg_entropy_kernel(JpegArgs a) {
   __shared__ K1Shared KS;
-  const int wv = threadIdx.x / JT;  // image (wave) within the workgroup
-  const int t = threadIdx.x % JT;
-  const int k = blockIdx.x * JW + wv;
-  JShared &S = KS.w[wv];
+  const int wi = threadIdx.x / JL;  // image within the workgroup
+  const int t = threadIdx.x % JL;   // lane within the image's segment
+  const int sg = (threadIdx.x % JT) / JL;  // segment within the wave
+  const int k = blockIdx.x * (JW * IPW) + wi;
+  JShared &S = KS.w[wi];
   const bool have = k < a.batch;
   ffcv_sample smp = {};
   if (have) smp = a.samples[k];
@@ -1018,7 +1060,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     if (MODE == JM_FULL) {  // zero-fill (K2 does it for RRC)
       uint64_t bytes = (uint64_t)smp.height * smp.width * 3;
       uint8_t *o = (uint8_t *)a.out + a.out_stride * k;
-      for (uint64_t i = t; i < bytes && i < a.out_stride; i += JT) o[i] = 0;
+      for (uint64_t i = t; i < bytes && i < a.out_stride; i += JL) o[i] = 0;
     }
   };
 
@@ -1031,8 +1073,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     const uint32_t *aw = (const uint32_t *)(src - mis);
     constexpr int NW = (HDR_BYTES + 4) / 4;
 #pragma unroll
-    for (int r = 0; r < (NW + JT - 1) / JT; r++) {
-      const int i = r * JT + t;
+    for (int r = 0; r < (NW + JL - 1) / JL; r++) {
+      const int i = r * JL + t;
       const int b0 = 4 * i - (int)mis;
       const uint32_t w = i < NW && b0 < (int)nh ? __builtin_nontemporal_load(aw + i) : 0u;
 #pragma unroll
@@ -1052,16 +1094,16 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   STAMP(1);
   int ref = -1;
 #pragma unroll
-  for (int w = JW - 1; w >= 0; w--)
+  for (int w = JW * IPW - 1; w >= 0; w--)
     if (KS.w[w].status == FFCV_SAMPLE_OK) ref = w;
   bool match = false;
   if (ref >= 0 && S.status == FFCV_SAMPLE_OK) {
     const JShared &R = KS.w[ref];
-    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * JW + ref].offset;
+    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * (JW * IPW) + ref].offset;
     match = R.nslots == S.nslots;
     for (int q = 0; q < NSLOT; q++)
       if (q < R.nslots && R.slot_tab[q] != S.slot_tab[q]) match = false;
-    if (match && ref != wv) {
+    if (match && ref != wi) {
       bool diff = false;
       for (int q = 0; q < R.nslots; q++) {
         const uint32_t dr = R.dht_off[R.slot_tab[q]], ds = S.dht_off[S.slot_tab[q]];
@@ -1070,14 +1112,14 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
         };
         int total = 0;
         for (int l = 0; l < 16; l++) total += hb(S, src, ds + l);
-        for (int i = t; i < 16 + total; i += JT) diff |= hb(S, src, ds + i) != hb(R, rsrc, dr + i);
+        for (int i = t; i < 16 + total; i += JL) diff |= hb(S, src, ds + i) != hb(R, rsrc, dr + i);
       }
-      match = !__any(diff);
+      match = !seg_any(diff, sg);
     }
   }
   if (ref >= 0) {
     const JShared &R = KS.w[ref];
-    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * JW + ref].offset;
+    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * (JW * IPW) + ref].offset;
     auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)__builtin_nontemporal_load(rsrc + p); };
     build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
   }
@@ -1096,8 +1138,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     return v;
   };
   JTables *gt = (JTables *)(a.gtab + a.gtab_slot * k);
-  if (!match) build_tables<JT>(*gt, S, HB, t);
-  for (int i = t; i < S.ncomp * 64; i += JT) {
+  if (!match) build_tables<JL>(*gt, S, HB, t);
+  for (int i = t; i < S.ncomp * 64; i += JL) {
     int c = i >> 6, zz = i & 63;
     int tq = S.tq[c];
     uint32_t q = S.dqt_off[tq];
@@ -1139,7 +1181,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     auto flush = [&](uint32_t upto) {  // write stage bytes [fbase, upto), upto % 4 == 0
       wsync_lds();
       const uint32_t nd = (upto - fbase) / 4;
-      for (uint32_t q = t; q < nd; q += JT) ((uint32_t *)gds)[fbase / 4 + q] = ((const uint32_t *)S.stage)[q];
+      for (uint32_t q = t; q < nd; q += JL) ((uint32_t *)gds)[fbase / 4 + q] = ((const uint32_t *)S.stage)[q];
       wsync_lds();
     };
     // DS_DEPTH-deep prefetch ring, unrolled so every ring register is consumed in
@@ -1147,25 +1189,25 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     auto ld = [&](uint32_t d) -> uint32_t { return d < ndw ? __builtin_nontemporal_load(aw + d) : 0u; };
     uint32_t r[DS_DEPTH];
 #pragma unroll
-    for (int u = 0; u < DS_DEPTH; u++) r[u] = ld(u * JT + t);
+    for (int u = 0; u < DS_DEPTH; u++) r[u] = ld(u * JL + t);
     int step = 0;
     bool done = false;
-    for (uint32_t base4 = 0; !done; base4 += DS_DEPTH * JT) {
+    for (uint32_t base4 = 0; !done; base4 += DS_DEPTH * JL) {
 #pragma unroll
       for (int u = 0; u < DS_DEPTH; u++) {
-        const uint32_t base = base4 + u * JT;
+        const uint32_t base = base4 + u * JL;
         if (done || base >= ndw) {
           done = true;
           continue;
         }
         const uint32_t di = base + t;
         const uint32_t w = r[u];
-        r[u] = ld(base + DS_DEPTH * JT + t);
+        r[u] = ld(base + DS_DEPTH * JL + t);
         const uint32_t wprev = lane_prev(w);
         const uint32_t wnext = lane_next(w);
-        const uint32_t nfirst = lane_read(r[(u + 1) % DS_DEPTH], 0);  // next step's first dword
+        const uint32_t nfirst = seg_read(r[(u + 1) % DS_DEPTH], 0, sg);  // next step's first dword
         const uint32_t prevb = t == 0 ? carry : (wprev >> 24);
-        const uint32_t next0 = (t == JT - 1 ? nfirst : wnext) & 0xff;
+        const uint32_t next0 = (t == JL - 1 ? nfirst : wnext) & 0xff;
         // SWAR over the 4 bytes (byte j = stream byte 4*di + j - mis):
         // zm(x) has 0x80 in every byte of x that is zero
         auto zm = [](uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
@@ -1185,22 +1227,22 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
         const int first_mk = mark4 ? __builtin_ctz(mark4) : 4;
         uint32_t keepm = valid4 & ~removed4 & ((1u << first_mk) - 1u);
         // the first marker of the step ends the segment
-        const uint64_t mk = __ballot(first_mk < 4);
+        const uint64_t mk = seg_ballot(first_mk < 4, sg);
         if (mk) {
           const int ml = __ffsll((unsigned long long)mk) - 1;
           if (t > ml) keepm = 0;
           done = true;
         }
         const uint32_t cnt = __popc(keepm);
-        uint32_t off = dlen + wave_exscan(cnt) - fbase;
+        uint32_t off = dlen + seg_exscan(cnt) - fbase;
 #pragma unroll
         for (int j = 0; j < 4; j++) {  // branch-free: dropped bytes go to a dummy byte
           const bool kj = (keepm >> j) & 1;
           S.stage[kj ? off + __popc(keepm & ((1u << j) - 1u)) : STAGE_DUMMY] = (uint8_t)(w >> (8 * j));
         }
         off += cnt;
-        dlen = lane_read(off, JT - 1) + fbase;
-        carry = lane_read(w, JT - 1) >> 24;
+        dlen = seg_read(off, JL - 1, sg) + fbase;
+        carry = seg_read(w, JL - 1, sg) >> 24;
       }
       if (!done && (step += DS_DEPTH) == DS_FLUSH) {  // flush whole dwords, keep the 0..3-byte tail
         step = 0;
@@ -1213,7 +1255,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
     // tail + zero padding (libjpeg fills zeros after a marker)
     wsync_lds();
-    for (uint32_t i = dlen - fbase + t; i < dlen - fbase + STREAM_PAD + 4; i += JT) S.stage[i] = 0;
+    for (uint32_t i = dlen - fbase + t; i < dlen - fbase + STREAM_PAD + 4; i += JL) S.stage[i] = 0;
     flush((dlen + STREAM_PAD + 3) & ~3u);
   }
   wsync_mem();
@@ -1222,8 +1264,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 
 
   int16_t *dcd = a.dcd + a.dcd_slot * k;
-  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, words, total_bits, coef, dcd)
-                             : entropy_passes(S, *gt, a, k, t, words, total_bits, coef, dcd);
+  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd)
+                             : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd);
   wsync_mem();
 
   // ------------------------------------------------------------- P6 ----
@@ -1232,7 +1274,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   STAMP(6);
   {
     const int nb = S.nblocks;
-    const int per_b = (nb + JT - 1) / JT;
+    const int per_b = (nb + JL - 1) / JL;
     const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
     int32_t s0 = 0, s1 = 0, s2 = 0;  // (registers: no dynamically indexed arrays)
     int ph = b0 % S.bpm;
@@ -1244,7 +1286,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       s2 += c == 2 ? d : 0;
       if (++ph == S.bpm) ph = 0;
     }
-    int32_t p0 = wave_exscan_i(s0), p1 = wave_exscan_i(s1), p2 = wave_exscan_i(s2);
+    int32_t p0 = seg_exscan_i(s0), p1 = seg_exscan_i(s1), p2 = seg_exscan_i(s2);
     ph = b0 % S.bpm;
     int m = b0 / S.bpm;
     int my = m / S.mcux, mx = m - my * S.mcux;
@@ -1271,7 +1313,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 
   if (MODE == JM_COEF) {
     int16_t *o = (int16_t *)a.out + a.out_stride / 2 * k;
-    for (int64_t b = t; b < S.nblocks; b += JT) {
+    for (int64_t b = t; b < S.nblocks; b += JL) {
       int64_t m = b / S.bpm;
       int ph = (int)(b - m * S.bpm);
       int my = (int)(m / S.mcux), mx = (int)(m - (int64_t)my * S.mcux);
@@ -1335,7 +1377,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 #pragma unroll
     for (int c = 0; c < 3; c++) nb[c] = c < S.ncomp ? (S.wx1[c] - S.wx0[c] + 1) * (S.wy1[c] - S.wy0[c] + 1) : 0;
     const int ntot = nb[0] + nb[1] + nb[2];
-    for (int i = t; i < ntot; i += JT) {
+    for (int i = t; i < ntot; i += JL) {
       int c = 0, j = i;
       if (j >= nb[0]) {
         j -= nb[0];
@@ -2061,7 +2103,7 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   const char *only_s = getenv("FFCV_JPEG_ONLY");
   const int only = only_s ? atoi(only_s) : 7;
   if (only & 1) {
-    hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0, s, a);
+    hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
@@ -2087,7 +2129,7 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   a.out = out;
   a.out_stride = out_stride;
   hipStream_t s = ffcv::as_stream(stream);
-  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0, s, a);
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
   dim3 g2((c->max_h + BAND - 1) / BAND, batch);
   hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_FULL, false>), g2, dim3(K2T), 0, s, a);
@@ -2105,7 +2147,7 @@ int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *
   a.out = coefs;
   a.out_stride = max_blocks * 64 * 2;
   a.max_blocks = max_blocks;
-  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3((batch + JW - 1) / JW), dim3(JW * JT), 0,
+  hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0,
                      ffcv::as_stream(stream), a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<COEF>");
   return FFCV_OK;

@@ -56,6 +56,7 @@ typedef struct {
 #define MAXEV 4096
 typedef struct {
   uint32_t ev[MAXEV];
+  uint32_t idx[MAXEV];  // blocks started before event q in this trajectory
   int nev;
   uint32_t cnt;  // blocks started from ev[0] on (or all if no drop)
   St exit;
@@ -65,12 +66,18 @@ static int heur = 0;
 static long steps;
 
 static uint32_t rec_from = 0;  // events / counts only at positions >= rec_from
+// SIM_NEV: events kept per trajectory (0 = all); SIM_SPARSE=1: the kept
+// events are the first block starts at or after NEV checkpoints spread over
+// the lane range [rng_lo, end) instead of the first NEV block starts
+static int nev_max = 0, sparse = 0;
+static uint32_t rng_lo = 0;
 static St run(St s, uint32_t end, Traj *t, const Traj *old, int spec) {
   int z = s.z, ph = s.ph;
   uint32_t pos = s.pos;
   uint32_t started = 0;
-  int n = 0, j = 0;
-  Traj nt;
+  int n = 0, j = 0, ck = 0;
+  const int cap = nev_max ? nev_max : MAXEV;
+  static Traj nt;
   nt.nev = 0;
   while (pos < end) {
     if (z == 0) {
@@ -78,16 +85,30 @@ static St run(St s, uint32_t end, Traj *t, const Traj *old, int spec) {
       if (old) {
         while (j < old->nev && old->ev[j] < key) j++;
         if (j < old->nev && old->ev[j] == key) {
-          for (int q = j; q < old->nev && n < MAXEV; q++) nt.ev[n++] = old->ev[q];
+          for (int q = j; q < old->nev && n < cap; q++) {
+            nt.ev[n] = old->ev[q];
+            nt.idx[n++] = started + old->idx[q] - old->idx[j];
+          }
           nt.nev = n;
-          nt.cnt = started + old->cnt - j;
+          nt.cnt = started + old->cnt - old->idx[j];
           nt.exit = old->exit;
           *t = nt;
           return nt.exit;
         }
       }
       if (pos >= rec_from) {
-        if (n < MAXEV) nt.ev[n++] = key;
+        int rec = n < cap;
+        if (sparse && nev_max) {
+          uint32_t ckpos = rng_lo + (uint32_t)((uint64_t)(end - rng_lo) * ck / nev_max);
+          rec = ck < nev_max && pos >= ckpos;
+          if (rec) {
+            while (ck < nev_max && pos >= rng_lo + (uint32_t)((uint64_t)(end - rng_lo) * ck / nev_max)) ck++;
+          }
+        }
+        if (rec && n < MAXEV) {
+          nt.ev[n] = key;
+          nt.idx[n++] = started;
+        }
         started++;
       }
     }
@@ -162,6 +183,8 @@ int main(int argc, char **argv) {
   fclose(f);
   int lanes = argc > 2 ? atoi(argv[2]) : 256;
   heur = argc > 3 ? atoi(argv[3]) : 0;
+  if (getenv("SIM_NEV")) nev_max = atoi(getenv("SIM_NEV"));
+  if (getenv("SIM_SPARSE")) sparse = atoi(getenv("SIM_SPARSE"));
   long p = 2;
   int hs[3], vs[3], cid[3], nc = 0, scan = 0;
   while (!scan) {
@@ -292,6 +315,7 @@ int main(int argc, char **argv) {
     St st0 = g[t];
     st0.pos = t * cb > (uint32_t)warm ? t * cb - warm : 0;
     rec_from = t * cb;
+    rng_lo = t * cb;
     run(t == 0 ? g[t] : st0, t == lanes - 1 ? tbits : (t + 1) * cb, &T[t], NULL, t > 0);
     rec_from = 0;
     if (steps > maxs) maxs = steps;
@@ -324,6 +348,7 @@ int main(int argc, char **argv) {
         NT[t].cnt = 0;
         NT[t].exit = ng[t];
       } else {
+        rng_lo = t * cb;
         run(ng[t], end, &NT[t], &T[t], 0);
       }
       if (steps > rm) rm = steps;

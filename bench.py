@@ -139,6 +139,9 @@ def main():
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)
+    ap.add_argument('--batch', type=int, default=0, help='diagnostic: override the config batch size')
+    ap.add_argument('--unfused', action='store_true',
+                    help='separate gather / draw kernels before the decode (the Loader\'s staged path)')
     ap.add_argument('--only', type=int, default=0,
                     help='diagnostic: timed steps launch only these decode kernels (bit 0 K1, bit 2 K2)')
     ap.add_argument('--inflight', type=int, default=16,
@@ -173,6 +176,8 @@ def main():
     from ffcv_amd import libffcv as L
 
     mode, side, out, batch, cut, norm, default_n = CONFIGS[args.config]
+    if args.batch:  # diagnostic: launch granularity (not the BASELINE config)
+        batch = args.batch
     N = args.dataset_size or default_n
     workers = max(1, min(16, cpu_threads() // max(1, world)))
     if local == 0:
@@ -252,6 +257,15 @@ def main():
         sl = slots[i % K]
         stream = streams[i % K]
         ids = d_order[i * batch:(i + 1) * batch]
+        if sl['dec'] is not None and not args.unfused:
+            # gather + draws fused into the entropy kernel (ffcv_jpeg_rrc_fused)
+            if ev is not None:
+                ev[0].record(stream)
+            sl['dec'].rrc_fused(d_data, d_table, ids, dp, sl['crops'], sl['cut'], None, rp, sl['out'],
+                                sl['status'], stream=stream)
+            if ev is not None:
+                ev[1].record(stream)
+            return
         L.gather_samples(d_table, ids, sl['smp'], stream)
         L.draw_batch(ids, sl['smp'], dp, sl['crops'], sl['cut'], None, sl['rstat'], stream)
         if ev is not None:

@@ -174,6 +174,43 @@ FFCV_DEV void center_crop(uint32_t height, uint32_t width, double ratio, int32_t
   out[3] = (int32_t)c;
 }
 
+// The draws of one sample under the seeding contract: part 0 =
+// crop (rgb_image.py:48-81) -> crops[4k..], part 1 = cutout origin
+// (cutout.py:38-42) -> cut[2k..], part 2 = flip (flip.py:35) -> flips[k].
+// Returns 1 when the MT19937 stream ran out (FFCV_SAMPLE_RNG).
+FFCV_DEV int draw_part(int part, int k, uint64_t id, uint32_t H, uint32_t W, const ffcv_draw_params &p,
+                       int32_t *crops, int32_t *cut, uint8_t *flips) {
+  DevMT m;
+  if (part == 0 && crops) {
+    int32_t c[4];
+    int err = 0;
+    if (p.crop_kind == 0) {
+      mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 1));
+      random_crop(m, H, W, p.scale, p.ratio, c);
+      err = m.err;
+    } else {
+      center_crop(H, W, p.center_ratio, c);
+    }
+    crops[4 * k + 0] = c[0];
+    crops[4 * k + 1] = c[1];
+    crops[4 * k + 2] = c[2];
+    crops[4 * k + 3] = c[3];
+    return err;
+  }
+  if (part == 1 && cut && p.cutout_size > 0) {
+    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 2));
+    cut[2 * k + 0] = (int32_t)mt_randint(m, p.out_h - p.cutout_size + 1);
+    cut[2 * k + 1] = (int32_t)mt_randint(m, p.out_w - p.cutout_size + 1);
+    return m.err;
+  }
+  if (part == 2 && flips) {
+    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 3));
+    flips[k] = (uint8_t)(mt_double(m) < p.flip_prob);
+  }
+  return 0;
+}
+
+
 // --------------------------------------------------------------------------
 // OpenCV 4.5.4 cv::resize(ROI, dst, dsize, 0, 0, INTER_AREA), CV_8UC3
 // (libffcv.cpp:33-42), restated per OUTPUT PIXEL so one lane computes one

@@ -121,6 +121,7 @@ struct JTables {
 // Per-image (per-wave) state.
 struct JShared {
   int status;
+  const uint8_t *src;  // the image's bytes (read by the workgroup's table build)
   int W, H, ncomp, hmax, vmax;
   int hs[3], vs[3], tq[3], td[3], ta[3], cid[3];
   int color_rgb;
@@ -570,6 +571,9 @@ struct JpegArgs {
   const int32_t *crops;
   const int32_t *cut;
   const uint8_t *flips;
+  int32_t *crops_w;  // the same arrays, written by the fused draws
+  int32_t *cut_w;
+  uint8_t *flips_w;
   ffcv_rrc_params p;
   void *out;
   uint64_t out_stride;
@@ -587,6 +591,14 @@ struct JpegArgs {
   uint8_t *gtab;  // per-image JTables for images that cannot share the workgroup's
   uint64_t gtab_slot;
   int batch;
+  // fused gather + draws (ffcv_jpeg_rrc_fused): samples = table[ids[k]],
+  // crop / cutout / flip drawn in K1 (lanes 1-3) into crops / cut / flips
+  const ffcv_sample *table;
+  uint64_t n_table;
+  const uint64_t *ids;
+  ffcv_sample *samples_out;
+  ffcv_draw_params dp;
+  int do_draw;
   uint32_t max_h, max_w;
   uint64_t max_blocks;
   uint64_t *dbg;
@@ -1043,7 +1055,24 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   JShared &S = KS.w[wi];
   const bool have = k < a.batch;
   ffcv_sample smp = {};
-  if (have) smp = a.samples[k];
+  int rng_err = 0;
+  if (have) {
+    if (a.table) {  // fused gather (gather_samples_kernel) + draws (draw_kernel)
+      const uint64_t id = a.ids[k];
+      if (id < a.n_table) {
+        smp = a.table[id];
+      } else {  // out-of-range index: an empty jpg sample -> BAD_MARKER status
+        smp.height = smp.width = 1;
+      }
+      if (t == 0 && a.samples_out) a.samples_out[k] = smp;
+      if (a.do_draw && t >= 1 && t <= 3)
+        rng_err = draw_part(t - 1, k, id, smp.height, smp.width, a.dp, a.crops_w, a.cut_w, a.flips_w);
+      rng_err = seg_any(rng_err != 0, sg);
+      wsync_mem();  // the crop (lane 1) is read by parse_header (lane 0)
+    } else {
+      smp = a.samples[k];
+    }
+  }
   ImgInfo *info = a.info + k;
   const bool live = have && smp.mode == 0;
   if (have && smp.mode != 0 && t == 0) {  // raw samples are handled by rrc_raw_kernel / gather
@@ -1085,7 +1114,10 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
   }
   wsync_lds();
-  if (t == 0) S.status = live ? parse_header(S, src, nbytes, smp, a, k, MODE) : -1;
+  if (t == 0) {
+    S.src = src;
+    S.status = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, src, nbytes, smp, a, k, MODE)) : -1;
+  }
   __syncthreads();
 
   // ------------------------------------------------------------- P1 ----
@@ -1099,7 +1131,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   bool match = false;
   if (ref >= 0 && S.status == FFCV_SAMPLE_OK) {
     const JShared &R = KS.w[ref];
-    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * (JW * IPW) + ref].offset;
+    const uint8_t *rsrc = R.src;
     match = R.nslots == S.nslots;
     for (int q = 0; q < NSLOT; q++)
       if (q < R.nslots && R.slot_tab[q] != S.slot_tab[q]) match = false;
@@ -1119,7 +1151,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   }
   if (ref >= 0) {
     const JShared &R = KS.w[ref];
-    const uint8_t *rsrc = a.base + a.samples[blockIdx.x * (JW * IPW) + ref].offset;
+    const uint8_t *rsrc = R.src;
     auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)__builtin_nontemporal_load(rsrc + p); };
     build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
   }
@@ -2078,26 +2110,13 @@ static int check_common(const char *fn, ffcv_jpeg_ctx *c, const uint8_t *base, c
   return FFCV_OK;
 }
 
-int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, const ffcv_sample *samples,
-                        int batch, const int32_t *crops, const int32_t *cutout_yx, const uint8_t *flips,
-                        const ffcv_rrc_params *p, void *out, int32_t *status) {
-  int rc = check_common("ffcv_jpeg_rrc_batch", c, base, samples, batch, out, status);
-  if (rc) return rc;
-  if (!p || !crops || p->out_h <= 0 || p->out_w <= 0) {
-    ffcv::set_error("ffcv_jpeg_rrc_batch: invalid params");
-    return FFCV_EINVAL;
-  }
-  if (batch == 0) return FFCV_OK;
-  JpegArgs a = make_args(c, base, samples, batch, status);
-  a.crops = crops;
-  a.cut = cutout_yx;
-  a.flips = flips;
+static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void *out) {
+  const int batch = a.batch;
   a.p = *p;
   a.out = out;
   const bool fp16 = p->lut != nullptr;
   uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
   a.out_stride = p->out_stride ? p->out_stride : dense;
-  hipStream_t s = ffcv::as_stream(stream);
   // diagnostics only (timing of one kernel re-run on the previous batch's
   // scratch): FFCV_JPEG_ONLY bit 0 = K1, bit 2 = K2
   const char *only_s = getenv("FFCV_JPEG_ONLY");
@@ -2114,6 +2133,54 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, false>), g2, dim3(K2T), K2_LDS, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<RRC>");
   return FFCV_OK;
+}
+
+int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, const ffcv_sample *samples,
+                        int batch, const int32_t *crops, const int32_t *cutout_yx, const uint8_t *flips,
+                        const ffcv_rrc_params *p, void *out, int32_t *status) {
+  int rc = check_common("ffcv_jpeg_rrc_batch", c, base, samples, batch, out, status);
+  if (rc) return rc;
+  if (!p || !crops || p->out_h <= 0 || p->out_w <= 0) {
+    ffcv::set_error("ffcv_jpeg_rrc_batch: invalid params");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  JpegArgs a = make_args(c, base, samples, batch, status);
+  a.crops = crops;
+  a.cut = cutout_yx;
+  a.flips = flips;
+  return launch_rrc(a, ffcv::as_stream(stream), p, out);
+}
+
+int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, const ffcv_sample *table,
+                        uint64_t n_table, const uint64_t *ids, int batch, const ffcv_draw_params *dp,
+                        int32_t *crops, int32_t *cutout_yx, uint8_t *flips, ffcv_sample *samples_out,
+                        const ffcv_rrc_params *p, void *out, int32_t *status) {
+  if (!c || !base || !table || !ids || !dp || !crops || !out || !status || batch < 0 || !p || p->out_h <= 0 ||
+      p->out_w <= 0) {
+    ffcv::set_error("ffcv_jpeg_rrc_fused: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  if (batch > c->max_batch) {
+    ffcv::set_error("ffcv_jpeg_rrc_fused: batch %d exceeds ctx max_batch %d", batch, c->max_batch);
+    return FFCV_EINVAL;
+  }
+  if (dp->out_h != p->out_h || dp->out_w != p->out_w || (cutout_yx && dp->cutout_size != p->cutout_size)) {
+    ffcv::set_error("ffcv_jpeg_rrc_fused: draw and resize parameters disagree");
+    return FFCV_EINVAL;
+  }
+  if (batch == 0) return FFCV_OK;
+  JpegArgs a = make_args(c, base, nullptr, batch, status);
+  a.table = table;
+  a.n_table = n_table;
+  a.ids = ids;
+  a.samples_out = samples_out;
+  a.dp = *dp;
+  a.do_draw = 1;
+  a.crops = a.crops_w = crops;
+  a.cut = a.cut_w = cutout_yx;
+  a.flips = a.flips_w = flips;
+  return launch_rrc(a, ffcv::as_stream(stream), p, out);
 }
 
 int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, const ffcv_sample *samples,

@@ -18,36 +18,10 @@ __global__ void __launch_bounds__(64) draw_kernel(const uint64_t *__restrict__ i
                                                   int32_t *__restrict__ status) {
   int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= B) return;
-  uint64_t id = ids[k];
+  const uint64_t id = ids[k];
+  const uint32_t H = crops ? samples[k].height : 0, W = crops ? samples[k].width : 0;
   int err = 0;
-  DevMT m;
-  if (crops) {
-    uint32_t H = samples[k].height, W = samples[k].width;
-    int32_t c[4];
-    if (p.crop_kind == 0) {
-      mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 1));
-      random_crop(m, H, W, p.scale, p.ratio, c);
-      err |= m.err;
-    } else {
-      center_crop(H, W, p.center_ratio, c);
-    }
-    crops[4 * k + 0] = c[0];
-    crops[4 * k + 1] = c[1];
-    crops[4 * k + 2] = c[2];
-    crops[4 * k + 3] = c[3];
-  }
-  if (cut && p.cutout_size > 0) {
-    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 2));
-    cut[2 * k + 0] = (int32_t)mt_randint(m, p.out_h - p.cutout_size + 1);
-    cut[2 * k + 1] = (int32_t)mt_randint(m, p.out_w - p.cutout_size + 1);
-    err |= m.err;
-  }
-  if (flips) {
-    // flip.py:35 rand() < flip_prob, one draw per sample under the contract
-    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 3));
-    double u = mt_double(m);
-    flips[k] = (uint8_t)(u < p.flip_prob);
-  }
+  for (int part = 0; part < 3; part++) err |= draw_part(part, k, id, H, W, p, crops, cut, flips);
   if (status) status[k] = err ? FFCV_SAMPLE_RNG : FFCV_SAMPLE_OK;
 }
 

@@ -217,13 +217,25 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
             out, smp, crops, cyx, flips, status = storage
             B = len(batch_indices)
             stream = ss.stream
-            samples = ss.batch_samples(f_ix, smp)
             dp = self._draw_params(ss)
-            L.draw_batch(ss.batch_ids, samples, dp, crops, cyx if cut is not None else None,
-                         flips if use_flip else None, None, stream)
             if norm is not None:
                 rp.lut = norm.device_lut(out.device).data_ptr()
             rp.out_stride = out[0].numel() * out.element_size()
+            if ss.dataset.data is not None and ss.any_mode(f_ix, 0):
+                # HBM-resident dataset: gather + draws run inside the entropy
+                # kernel (ffcv_jpeg_rrc_fused), two fewer launches per batch
+                dec = ss.jpeg_decoder(f_ix)
+                dec.rrc_fused(ss.data, ss.sample_table(f_ix), ss.batch_ids, dp, crops,
+                              cyx if cut is not None else None, flips if use_flip else None, rp, out,
+                              status, samples_out=smp, stream=stream)
+                ss.check_status(status[:B], type(self).__name__)
+                if ss.any_mode(f_ix, 1):
+                    L.rrc_raw_batch(ss.data, smp[:B], B, crops, cyx if cut is not None else None,
+                                    flips if use_flip else None, rp, out, stream)
+                return out[:B]
+            samples = ss.batch_samples(f_ix, smp)
+            L.draw_batch(ss.batch_ids, samples, dp, crops, cyx if cut is not None else None,
+                         flips if use_flip else None, None, stream)
             if ss.any_mode(f_ix, 1):
                 L.rrc_raw_batch(ss.data, samples, B, crops, cyx if cut is not None else None,
                                 flips if use_flip else None, rp, out, stream)

@@ -84,6 +84,9 @@ _SIGS = {
     'ffcv_jpeg_destroy': (c_int, [c_void_p]),
     'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'ffcv_jpeg_rrc_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+                                    c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
     'ffcv_jpeg_decode_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                        c_uint64, c_void_p]),
     'ffcv_jpeg_coefficients_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
@@ -218,6 +221,15 @@ class JpegDecoder:
                                          int(batch), _p(crops), _p(cutout_yx), _p(flips),
                                          ctypes.byref(params), _p(out), _p(status)),
                'ffcv_jpeg_rrc_batch')
+
+    def rrc_fused(self, base, table, ids, draw: DrawParams, crops, cutout_yx, flips,
+                  params: RRCParams, out, status, samples_out=None, stream=None):
+        """gather + draws + decode/crop/resize/epilogue (ffcv_jpeg_rrc_fused)."""
+        _check(lib().ffcv_jpeg_rrc_fused(self.handle, _stream(stream), _p(base), _p(table),
+                                         table.numel() // 32, _p(ids), int(ids.shape[0]),
+                                         ctypes.byref(draw), _p(crops), _p(cutout_yx), _p(flips),
+                                         _p(samples_out), ctypes.byref(params), _p(out),
+                                         _p(status)), 'ffcv_jpeg_rrc_fused')
 
     def decode(self, base, samples, batch, out, out_stride, status, stream=None):
         _check(lib().ffcv_jpeg_decode_batch(self.handle, _stream(stream), _p(base), _p(samples),

@@ -171,6 +171,22 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *ctx, void *stream, const uint8_t *base,
                         const uint8_t *flips, const ffcv_rrc_params *p,
                         void *out, int32_t *status);
 
+/* ffcv_gather_samples + ffcv_draw_batch + ffcv_jpeg_rrc_batch in one launch
+ * sequence: the entropy kernel reads sample ids[k] of table[n_table] and
+ * draws its crop / cutout origin / flip under the seeding contract itself
+ * (two fewer small kernels on the slot's stream).  crops (int32[B,4]) is
+ * required; cutout_yx (int32[B,2]) and flips (uint8[B]) may be NULL; all
+ * three are written for the caller, like ffcv_draw_batch.  samples_out
+ * (ffcv_sample[B], may be NULL) receives the gathered descriptors, e.g. for
+ * ffcv_rrc_raw_batch on the raw samples of a mixed field.  An RNG overrun
+ * sets that sample's status to FFCV_SAMPLE_RNG. */
+int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *ctx, void *stream, const uint8_t *base,
+                        const ffcv_sample *table, uint64_t n_table,
+                        const uint64_t *ids, int batch, const ffcv_draw_params *dp,
+                        int32_t *crops, int32_t *cutout_yx, uint8_t *flips,
+                        ffcv_sample *samples_out, const ffcv_rrc_params *p,
+                        void *out, int32_t *status);
+
 /* rgb_image.py:123-136 SimpleRGBImageDecoder jpg branch (imdecode into the
  * destination, full image) -> device [B][H][W][3] with out_stride bytes per
  * sample. */

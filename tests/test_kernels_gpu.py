@@ -316,3 +316,66 @@ def test_jpeg_corrupt_and_unsupported(hip_lib, oracle):
     o = out.cpu().numpy()
     assert np.array_equal(o[0].reshape(64, 80, 3), oracle.jpeg_decode(good))
     assert (o[1] == 0).all() and (o[2] == 0).all()
+
+
+def test_jpeg_rrc_fused_matches_staged(hip_lib, oracle):
+    """ffcv_jpeg_rrc_fused (gather + draws inside the entropy kernel) gives the
+    same crops / cutout / flips / samples / pixels as gather -> draw -> rrc,
+    and the decode matches the oracle; an out-of-range id fails cleanly."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(31)
+    imgs, blobs = _jpeg_set(rng, 40)
+    buf, offs, sizes = pack(blobs)
+    hs = [i.shape[0] for i in imgs]
+    ws = [i.shape[1] for i in imgs]
+    table = _samples(offs, sizes, hs, ws, np.zeros(len(imgs)))
+    d_buf, d_table = _upload(buf), _dev(table)
+    ids = rng.permutation(len(imgs))[:33].astype(np.int64)
+    ids[5] = 10 ** 6  # out of range
+    B = len(ids)
+    d_ids = torch.from_numpy(ids).to('cuda:0')
+    dp = L.DrawParams()
+    dp.crop_kind = 0
+    dp.out_h = dp.out_w = 224
+    dp.cutout_size = 32
+    dp.scale[0], dp.scale[1] = 0.08, 1.0
+    dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
+    dp.loader_seed = 7
+    dp.epoch = 3
+    dp.flip_prob = 0.5
+    rp = L.RRCParams()
+    rp.out_h = rp.out_w = 224
+    rp.cutout_size = 32
+    for i, f in enumerate((124, 116, 103)):
+        rp.cutout_fill[i] = f
+    dec = L.JpegDecoder(B, max(hs), max(ws), max(len(b) for b in blobs))
+    res = []
+    for fused in (False, True):
+        crops = torch.full((B, 4), -7, dtype=torch.int32, device='cuda:0')
+        cut = torch.full((B, 2), -7, dtype=torch.int32, device='cuda:0')
+        flips = torch.full((B,), 9, dtype=torch.uint8, device='cuda:0')
+        smp = torch.zeros(B * 32, dtype=torch.uint8, device='cuda:0')
+        out = torch.zeros((B, 224, 224, 3), dtype=torch.uint8, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        if fused:
+            dec.rrc_fused(d_buf, d_table, d_ids, dp, crops, cut, flips, rp, out, status, samples_out=smp)
+        else:
+            L.gather_samples(d_table.view(-1, 32), d_ids, smp)
+            L.draw_batch(d_ids, smp, dp, crops, cut, flips)
+            dec.rrc(d_buf, smp, B, crops, cut, flips, rp, out, status)
+        torch.cuda.synchronize()
+        res.append([x.cpu().numpy() for x in (crops, cut, flips, smp, out, status)])
+    names = ['crops', 'cut', 'flips', 'samples', 'out', 'status']
+    for n, a_, b_ in zip(names, *res):
+        assert np.array_equal(a_, b_), n
+    st = res[1][5]
+    assert st[5] != 0 and (np.delete(st, 5) == 0).all()
+    assert (res[1][4][5] == 0).all()
+    # the decode itself against the oracle (two samples)
+    crops, cut, flips = res[1][0], res[1][1], res[1][2]
+    for k in (0, 17):
+        i = int(ids[k])
+        want = oracle.rrc_batch([(blobs[i], hs[i], ws[i], 0)], crops[k:k + 1], 224, 224)
+        want = _oracle_post(want, flips[k:k + 1], cut[k:k + 1], 32, (124, 116, 103))
+        assert np.array_equal(res[1][4][k], want[0]), k

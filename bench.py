@@ -295,6 +295,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, events[i])
+    host_s = time.perf_counter() - t0  # host submission time of the K steps
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -324,6 +325,7 @@ def main():
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+        'host_submit_ms_per_step': round(host_s / args.steps * 1e3, 4),
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,

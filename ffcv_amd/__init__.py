@@ -10,10 +10,16 @@ import os as _os
 
 # Batches in flight each run on their own HIP stream; with HIP's default of 4
 # hardware queues, streams beyond 3 share queues and serialise.  16 queues let
-# the Loader keep up to 8 batches in flight (the measured optimum on MI355X,
-# DESIGN.md section 6).  Only takes effect if set before the process's first
-# HIP call; a value the user already exported is kept.
-_os.environ.setdefault('GPU_MAX_HW_QUEUES', '16')
+# the Loader keep 8 batches in flight (the measured optimum on MI355X,
+# DESIGN.md section 6).  Raised to at least 16 -- environments commonly
+# export HIP's default of 4 -- and only effective before the process's first
+# HIP call.
+try:
+    _hwq = int(_os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+except ValueError:
+    _hwq = 4
+if _hwq < 16:
+    _os.environ['GPU_MAX_HW_QUEUES'] = '16'
 
 from .loader import Loader  # noqa: E402
 from .writer import DatasetWriter  # noqa: E402

@@ -1041,10 +1041,10 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 
 template <int MODE>
 // Waves per SIMD K1 is compiled for: 4 (= the LDS limit, 16 images per CU)
-// caps it at 128 VGPRs and spills a few; 3 measured equal or slightly faster
-// in the full pipeline (K2's workgroups share the CUs).
+// caps it at 128 VGPRs (a few spill, outside the decode loops); measured
+// 1-2% faster than 3 (143 VGPRs) in the full pipeline.
 #ifndef K1_WPE
-#define K1_WPE 3
+#define K1_WPE 4
 #endif
 __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1_WPE))) jpeg_entropy_kernel(JpegArgs a) {
   __shared__ K1Shared KS;

@@ -605,7 +605,8 @@ struct JpegArgs {
   int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs;
                 // timing only (wrong output): bit 3 skips the colour pass, bit 4 the resize arithmetic;
                 // bit 5 disables the separable linear resize, bit 6 the 4:2:0 quad colour pass,
-                // bit 7 the linear fast path
+                // bit 7 the linear fast path; timing only: bits 8 / 9 / 10 skip the fast
+                // path's colour pass / column walk / tile staging
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1659,7 +1660,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
         uint32_t *tl = (uint32_t *)(lds + toff[c]);
         const int wpr = tpitch[c] >> 2, n = trows[c] * wpr;
         const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
-        for (int i = t; i < n; i += K2T) {
+        for (int i = t; i < n && !(a.k2flags & 1024); i += K2T) {
           const int rr = i / wpr, q = i - rr * wpr;
           tl[i] = *(const uint32_t *)(src + (uint64_t)rr * gp[c].stride + 4 * q);
         }
@@ -1667,7 +1668,8 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       }
       __syncthreads();
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
-      if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
+      if (a.k2flags & 256) {
+      } else if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
           G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {
         // 4:2:0: one thread per chroma sample, its 2x2 pixel quad
         const int R0 = Y0 >> 1, C0 = X0 >> 1, qcols = (X1 >> 1) - C0 + 1;
@@ -1700,21 +1702,25 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       const int dx0 = 2 * tx;
       const LinTap l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
       const LinTap l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
+      // a border tap (src[s] * 2048) as the same two-tap form with weights
+      // (2048, 0) on (s, s): branch-free, identical sums
+      const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
+      const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
       // horizontal pass of crop row r for both columns: sat_s16(h >> 4) per channel
       auto hrow = [&](int r, int H[6]) {
         const uint32_t *row = rgbx + (r - r0) * rw;
-        const uint32_t p0 = row[l0.s], q0 = row[l0.border ? l0.s : l0.s + 1];
-        const uint32_t p1 = row[l1.s], q1 = row[l1.border ? l1.s : l1.s + 1];
+        const uint32_t p0 = row[l0.s], q0 = row[s0b];
+        const uint32_t p1 = row[l1.s], q1 = row[s1b];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
           const int a0 = (p0 >> (8 * c)) & 255, b0 = (q0 >> (8 * c)) & 255;
           const int a1 = (p1 >> (8 * c)) & 255, b1 = (q1 >> (8 * c)) & 255;
-          H[c] = sat_s16i((l0.border ? a0 * 2048 : a0 * l0.c0 + b0 * l0.c1) >> 4);
-          H[3 + c] = sat_s16i((l1.border ? a1 * 2048 : a1 * l1.c0 + b1 * l1.c1) >> 4);
+          H[c] = sat_s16i((a0 * a0w + b0 * b0w) >> 4);
+          H[3 + c] = sat_s16i((a1 * a1w + b1 * b1w) >> 4);
         }
       };
       const int half = (BAND + 1) / 2;
-      const int ya = oy0 + sub * half, yb = min(oy1, ya + half);
+      const int ya = oy0 + sub * half, yb = (a.k2flags & 512) ? ya : min(oy1, ya + half);
       int ca = -1, cb = -1;
       int HA[6], HB[6];
       for (int dy = ya; dy < yb; dy++) {

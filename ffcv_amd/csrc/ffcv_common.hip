@@ -5,6 +5,11 @@
 
 #include "api_internal.h"
 
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
 namespace ffcv {
 static thread_local std::string g_last_error;
 
@@ -70,5 +75,42 @@ int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stre
 
 // libffcv.cpp:44-46: my_memcpy(source, dst, size) -- host plumbing only.
 void my_memcpy(void *source, void *dst, uint64_t size) { std::memcpy(dst, source, size); }
+
+// Host gather of n byte ranges (e.g. a batch's compressed samples out of the
+// mmap'd .beton) into one staging buffer, split over nthreads threads by
+// byte count.  The PCIe path (device_cache=False) stages each batch this way
+// before one hipMemcpyAsync.
+int ffcv_host_gather(const uint8_t *src, const uint64_t *src_off, const uint64_t *sizes, const uint64_t *dst_off,
+                     int n, uint8_t *dst, int nthreads) {
+  if (n < 0 || (n > 0 && (!src || !src_off || !sizes || !dst_off || !dst))) {
+    ffcv::set_error("ffcv_host_gather: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  uint64_t total = 0;
+  for (int i = 0; i < n; i++) total += sizes[i];
+  const int T = std::max(1, std::min(nthreads, n));
+  auto work = [&](int tid) {
+    // contiguous runs of samples with about total / T bytes each
+    const uint64_t lo = total * tid / T, hi = total * (tid + 1) / T;
+    uint64_t acc = 0;
+    for (int i = 0; i < n; i++) {
+      const uint64_t a = acc, b = acc + sizes[i];
+      acc = b;
+      if (b <= lo || a >= hi) continue;
+      const uint64_t s = std::max(a, lo) - a, e = std::min(b, hi) - a;
+      std::memcpy(dst + dst_off[i] + s, src + src_off[i] + s, e - s);
+    }
+  };
+  if (T == 1) {
+    work(0);
+    return FFCV_OK;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+  return FFCV_OK;
+}
 
 }  // extern "C"

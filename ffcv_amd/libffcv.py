@@ -74,6 +74,7 @@ _SIGS = {
     'ffcv_memcpy_h2d_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     'ffcv_memcpy_d2h_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     'my_memcpy': (None, [c_void_p, c_void_p, c_uint64]),
+    'ffcv_host_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int]),
     'ffcv_draw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
     'ffcv_rrc_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
@@ -158,6 +159,16 @@ def _stream(stream):
 def memcpy(source: np.ndarray, dest: np.ndarray):
     """ffcv/libffcv.py:51-55 memcpy (host plumbing)."""
     lib().my_memcpy(source.ctypes.data, dest.ctypes.data, source.size * source.itemsize)
+
+
+def host_gather(src: np.ndarray, src_off: np.ndarray, sizes: np.ndarray, dst_off: np.ndarray, dst,
+                nthreads=8):
+    """Gather byte ranges of a host buffer (e.g. the mmap) into dst (numpy / pinned tensor)."""
+    so = np.ascontiguousarray(src_off, dtype=np.uint64)
+    sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+    do = np.ascontiguousarray(dst_off, dtype=np.uint64)
+    _check(lib().ffcv_host_gather(_p(src), _p(so), _p(sz), _p(do), int(len(sz)), _p(dst), int(nthreads)),
+           'ffcv_host_gather')
 
 
 def draw_batch(ids, samples, params: DrawParams, crops=None, cutout_yx=None, flips=None,

@@ -183,10 +183,9 @@ class BatchContext:
             self._staging[f_ix] = st
         host, dev, desc_host = st
         mm = self.host_state[0]
-        hv = host.numpy()
-        src = table['offset'].astype(np.int64)
-        for k in range(B):
-            hv[offs[k]:offs[k] + sizes[k]] = mm[src[k]:src[k] + sizes[k]]
+        # native multi-threaded gather out of the mmap (ffcv_host_gather)
+        L.host_gather(mm, table['offset'].astype(np.uint64) + np.uint64(self.dataset.data_base),
+                      sizes, offs, host, nthreads=min(8, max(1, B // 32)))
         t = table.copy()
         t['offset'] = offs.astype(np.uint64)
         desc_host[:B * 32].copy_(ch.from_numpy(t.view(np.uint8)))

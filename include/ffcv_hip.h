@@ -110,6 +110,13 @@ int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stre
  * CPU-only Loader, C1).  Same argument order as the reference. */
 void my_memcpy(void *source, void *dst, uint64_t size);
 
+/* Host gather of n byte ranges src + src_off[i] (sizes[i] bytes) to
+ * dst + dst_off[i], split over nthreads threads by bytes: the PCIe path's
+ * per-batch staging of compressed samples from the mmap'd .beton
+ * (memory_managers/os_cache.py:55-60 read, batched). */
+int ffcv_host_gather(const uint8_t *src, const uint64_t *src_off, const uint64_t *sizes,
+                     const uint64_t *dst_off, int n, uint8_t *dst, int nthreads);
+
 /* ------------------------------------------------------- random draws -- */
 /* rgb_image.py:48-81 crop windows (+ cutout.py:38-42 origins, + flip.py:35
  * decisions) for B samples, on the device.

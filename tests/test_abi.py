@@ -1,6 +1,8 @@
 """The C-ABI library builds for gfx950, loads, and exports every function
 include/ffcv_hip.h declares (CPU: no compute calls)."""
 import ctypes
+
+import numpy as np
 import os
 import re
 
@@ -47,3 +49,21 @@ def test_host_memcpy_and_errors(hip_lib):
     assert rc == -1 and b'invalid' in hip_lib.ffcv_last_error()
     rc = hip_lib.ffcv_jpeg_create(None, 0, 0, 0, 0)
     assert rc == -1
+
+
+def test_host_gather_cpu():
+    """ffcv_host_gather (the PCIe path's batch staging) on host memory only."""
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(0)
+    src = rng.integers(0, 256, 100000).astype(np.uint8)
+    so = rng.integers(0, 90000, 40).astype(np.uint64)
+    sizes = np.minimum(rng.integers(0, 3000, 40).astype(np.uint64), np.uint64(100000) - so)
+    sizes[3] = 0
+    do = np.zeros(40, np.uint64)
+    do[1:] = np.cumsum(sizes)[:-1]
+    for nt in (1, 3, 8):
+        dst = np.zeros(int(sizes.sum()) + 16, np.uint8)
+        L.host_gather(src, so, sizes, do, dst, nthreads=nt)
+        for i in range(40):
+            assert np.array_equal(dst[int(do[i]):int(do[i] + sizes[i])], src[int(so[i]):int(so[i] + sizes[i])])
+        assert not dst[int(sizes.sum()):].any()

@@ -48,8 +48,15 @@ FFCV_DEV void store_px(void *out, uint64_t idx, const int v[3], const uint16_t *
 }
 
 #define RRC_THREADS 256
-#define RRC_PPT 4
+#define RRC_BAND 16  // output rows per workgroup
 
+// One workgroup per band of RRC_BAND output rows of one image.
+//   Linear fast path (every crop upscaled along some axis, OpenCV's
+//   "area-mode" linear with the SSE2 vertical body on every element): each
+//   thread owns one output column pair and walks the band's rows, keeping
+//   the two source rows' horizontal sums in registers, so the column taps
+//   are computed once per thread and each source row once per column pair.
+//   Otherwise (area downscale, odd widths): the per-pixel restatement.
 template <bool FP16>
 __global__ void __launch_bounds__(RRC_THREADS)
     rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
@@ -57,13 +64,17 @@ __global__ void __launch_bounds__(RRC_THREADS)
                    const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
                    void *__restrict__ out) {
   __shared__ uint16_t s_lut[FP16 ? 768 : 1];
+  __shared__ LinTap s_rt[RRC_BAND];
   const int k = blockIdx.y;
+  const int t = threadIdx.x;
   const ffcv_sample s = samples[k];
   if (FP16) {
-    for (int i = threadIdx.x; i < 768; i += RRC_THREADS) s_lut[i] = p.lut[i];
+    for (int i = t; i < 768; i += RRC_THREADS) s_lut[i] = p.lut[i];
     __syncthreads();
   }
   if (s.mode != 1) return;
+  const int oy0 = blockIdx.x * RRC_BAND, oy1 = min(p.out_h, oy0 + RRC_BAND);
+  if (oy0 >= p.out_h) return;
   const int ci = crops[4 * k], cj = crops[4 * k + 1], chh = crops[4 * k + 2], cww = crops[4 * k + 3];
   GlobalSrc src{base + s.offset + ((uint64_t)ci * s.width + cj) * 3, (uint64_t)s.width * 3};
   ResizePlan P = make_plan(cww, chh, p.out_w, p.out_h);
@@ -78,14 +89,82 @@ __global__ void __launch_bounds__(RRC_THREADS)
   ep.fill[0] = p.cutout_fill[0];
   ep.fill[1] = p.cutout_fill[1];
   ep.fill[2] = p.cutout_fill[2];
-  const int npx = p.out_h * p.out_w;
   char *o = (char *)out + stride * k;
-  const int first = blockIdx.x * RRC_THREADS * RRC_PPT + threadIdx.x;
+  const int out_w = p.out_w;
+  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * RRC_THREADS) {
+    if (t < oy1 - oy0) s_rt[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+    __syncthreads();
+    if (t >= out_w / 2) return;
+    const int dx0 = 2 * t;
+    const LinTap l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
+    const LinTap l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
+    // a border tap (src[s] * 2048) as the two-tap form with weights (2048, 0)
+    const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
+    const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
+    auto hrow = [&](int r, int H[6]) {  // resize.cpp HResizeLinear of crop row r: sat_s16(h >> 4)
+      const uint8_t *row = src.p + (uint64_t)r * src.step;
 #pragma unroll
-  for (int r = 0; r < RRC_PPT; r++) {
-    int px = first + r * RRC_THREADS;
-    if (px >= npx) break;
-    int dy = px / p.out_w, dx = px - dy * p.out_w;
+      for (int c = 0; c < 3; c++) {
+        const int a0 = row[l0.s * 3 + c], b0 = row[s0b * 3 + c];
+        const int a1 = row[l1.s * 3 + c], b1 = row[s1b * 3 + c];
+        H[c] = sat_s16i((a0 * a0w + b0 * b0w) >> 4);
+        H[3 + c] = sat_s16i((a1 * a1w + b1 * b1w) >> 4);
+      }
+    };
+    int ca = -1, cb = -1;
+    int HA[6], HB[6];
+    for (int dy = oy0; dy < oy1; dy++) {
+      const LinTap ly = s_rt[dy - oy0];
+      const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
+      if (ra != ca) {
+        if (ra == cb) {
+#pragma unroll
+          for (int i = 0; i < 6; i++) HA[i] = HB[i];
+        } else {
+          hrow(ra, HA);
+        }
+        ca = ra;
+      }
+      if (rb != cb) {
+        hrow(rb, HB);
+        cb = rb;
+      }
+      int v[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) {  // VResizeLinearVec_32s8u
+        const int m0 = (HA[i] * ly.c0) >> 16, m1 = (HB[i] * ly.c1) >> 16;
+        v[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
+      }
+      if (ep.in_cut(dy, dx0)) {
+        v[0] = ep.fill[0];
+        v[1] = ep.fill[1];
+        v[2] = ep.fill[2];
+      }
+      if (ep.in_cut(dy, dx0 + 1)) {
+        v[3] = ep.fill[0];
+        v[4] = ep.fill[1];
+        v[5] = ep.fill[2];
+      }
+      const uint64_t px = (uint64_t)dy * out_w + dx0;
+      if (FP16) {  // 12-byte group, 4-byte aligned (dx0 even)
+        uint32_t *o32 = (uint32_t *)((uint16_t *)o + px * 3);
+        const uint32_t h0 = s_lut[v[0] * 3], h1 = s_lut[v[1] * 3 + 1], h2 = s_lut[v[2] * 3 + 2];
+        const uint32_t h3 = s_lut[v[3] * 3], h4 = s_lut[v[4] * 3 + 1], h5 = s_lut[v[5] * 3 + 2];
+        o32[0] = h0 | (h1 << 16);
+        o32[1] = h2 | (h3 << 16);
+        o32[2] = h4 | (h5 << 16);
+      } else {
+        uint16_t *o16 = (uint16_t *)((uint8_t *)o + px * 3);
+        o16[0] = (uint16_t)(v[0] | (v[1] << 8));
+        o16[1] = (uint16_t)(v[2] | (v[3] << 8));
+        o16[2] = (uint16_t)(v[4] | (v[5] << 8));
+      }
+    }
+    return;
+  }
+  const int npx = (oy1 - oy0) * out_w;
+  for (int i = t; i < npx; i += RRC_THREADS) {
+    const int dy = oy0 + i / out_w, dx = i % out_w;
     int v[3];
     if (ep.in_cut(dy, dx)) {
       v[0] = ep.fill[0];
@@ -94,7 +173,7 @@ __global__ void __launch_bounds__(RRC_THREADS)
     } else {
       resize_pixel(P, src, dy, ep.src_x(dx), v);
     }
-    store_px<FP16>(o, px, v, s_lut);
+    store_px<FP16>(o, (uint64_t)dy * out_w + dx, v, s_lut);
   }
 }
 
@@ -216,8 +295,7 @@ int ffcv_rrc_raw_batch(void *stream, const uint8_t *base, const ffcv_sample *sam
   const bool fp16 = p->lut != nullptr;
   uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
   uint64_t stride = p->out_stride ? p->out_stride : dense;
-  int npx = p->out_h * p->out_w;
-  dim3 grid((npx + RRC_THREADS * RRC_PPT - 1) / (RRC_THREADS * RRC_PPT), batch);
+  dim3 grid((p->out_h + RRC_BAND - 1) / RRC_BAND, batch);
   if (fp16)
     hipLaunchKernelGGL(rrc_raw_kernel<true>, grid, dim3(RRC_THREADS), 0, ffcv::as_stream(stream), base,
                        samples, crops, cutout_yx, flips, *p, stride, out);

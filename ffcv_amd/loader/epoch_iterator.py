@@ -63,7 +63,12 @@ class EpochIterator(Thread):
         except MemoryError as e:
             raise e
         self.storage_state = self.memory_context.state
-        n_slots = self.loader.batches_ahead + 2
+        # decode slots: at least batches_ahead + 2 (the reference's ring), and
+        # at least max_streams() so that many batches can be decoding at once
+        # (8 in flight measured fastest on MI355X); batches_ahead still bounds
+        # how far the producer runs ahead of the consumer (the output queue)
+        n_slots = max(self.loader.batches_ahead + 2, max_streams() if self.is_cuda else 0)
+        self.n_slots = n_slots
         # Slot state lives on the loader across epochs: the device buffers and
         # the JPEG decoder scratch (hundreds of MB per slot) are allocated
         # once, not per epoch.  The slots share at most max_streams() HIP
@@ -119,7 +124,7 @@ class EpochIterator(Thread):
             while True:
                 ixes = next(self.iter_ixes)
                 slot = self.current_batch_slot
-                self.current_batch_slot = (slot + 1) % (self.loader.batches_ahead + 2)
+                self.current_batch_slot = (slot + 1) % self.n_slots
                 t0 = time.perf_counter()
                 result = self.run_pipeline(b_ix, ixes, slot, events[slot])
                 self._t_pipeline += time.perf_counter() - t0
@@ -133,7 +138,7 @@ class EpochIterator(Thread):
                     if self.terminate_event.is_set():
                         return
                 if self.is_cuda:
-                    just_finished_slot = (slot - self.loader.batches_ahead - 1) % (self.loader.batches_ahead + 2)
+                    just_finished_slot = (slot - self.loader.batches_ahead - 1) % self.n_slots
                     event = ch.cuda.Event()
                     event.record(self.current_stream)
                     events[just_finished_slot] = event

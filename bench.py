@@ -133,8 +133,8 @@ def cpu_baseline(cfg, tile, offs, sizes, hs, ws, budget_s=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--steps', type=int, default=400)
+    ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='c3', choices=list(CONFIGS))
     ap.add_argument('--unique', type=int, default=4096)
     ap.add_argument('--dataset-size', type=int, default=None)

@@ -75,10 +75,12 @@
 #define DS_DEPTH 8      // de-stuff loads in flight per lane
 #define STAGE_DUMMY (2 * (NEV + 1) * JL * 4 - 4)
 #define STREAM_PAD 32   // zero bytes after the de-stuffed stream
-#define BAND 16
+#ifndef BAND
+#define BAND 16  // K2 output rows per workgroup
+#endif
 #define K2T 256
 #ifndef K2_LDS
-#define K2_LDS 32768
+#define K2_LDS 24576  // K2 dynamic LDS: 6 workgroups per CU; bigger bands take the general path (32 KB measured 3% slower)
 #endif
 #ifndef JW
 #define JW 4  // waves per K1 workgroup

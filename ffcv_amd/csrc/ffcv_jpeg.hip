@@ -62,18 +62,24 @@
 #endif
 #define IPW (JT / JL)   // images per wave
 #define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
-#define LUT_POOL 5121   // first-level LUT words shared by the slots (+ the zero word)
-#define FB_AC 11        // first-level bits, AC tables
-#define FB_DC 9         // first-level bits, DC tables
+#define FB_AC 11        // first-level bits, the scan's first AC table (luma)
+#define FB_AC2 10       // first-level bits, further AC tables (chroma)
+#define FB_DC 8         // first-level bits, DC tables
+// first-level LUT words shared by the slots (+ the zero word): one table of
+// each AC size and two DC tables, the 4:2:0 / 4:2:2 / 4:4:4 norm
+#define LUT_POOL ((1 << FB_AC) + (1 << FB_AC2) + 2 * (1 << FB_DC) + 1)
 #define SUBB 5          // second-level bits
 #define NSUB 8          // second-level tables per slot
 #define NSLOT 6         // Huffman tables a scan can reference (3 DC + 3 AC)
 #define NLUTSLOT 4      // slots that can get a first-level LUT from the pool
 #define NTAB 8
-#define NEV 8
-#define DS_FLUSH 16     // de-stuff steps per LDS -> HBM flush
+#ifndef NEV
+#define NEV 6
+#endif
+#define DS_FLUSH 8      // de-stuff steps per LDS -> HBM flush
 #define DS_DEPTH 8      // de-stuff loads in flight per lane
-#define STAGE_DUMMY (2 * (NEV + 1) * JL * 4 - 4)
+#define STAGE_BYTES (DS_FLUSH * JL * 4 + 64)  // a flush's bytes + the carried tail + pad
+#define STAGE_DUMMY (STAGE_BYTES - 4)
 #define STREAM_PAD 32   // zero bytes after the de-stuffed stream
 #ifndef BAND
 #define BAND 16  // K2 output rows per workgroup
@@ -117,7 +123,7 @@ struct JTables {
   uint16_t sub_prefix[NSLOT][NSUB];
   // second-level tables (codes longer than the first level; make_entry format)
   uint16_t lut2[NLUTSLOT][NSUB][1 << SUBB];
-  uint16_t lut[LUT_POOL];  // first-level LUT pool
+  uint32_t lut[LUT_POOL];  // first-level LUT pool (single or pair entries, see make_pair)
 };
 
 // Per-image (per-wave) state.
@@ -158,7 +164,7 @@ struct JShared {
   union {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
     uint32_t ev[2][NEV + 1][JL];  // P3: block-start events (pos << 4 | phase), double-buffered
-    uint8_t stage[2 * (NEV + 1) * JL * 4];  // P2: de-stuffed bytes awaiting a flush
+    uint8_t stage[STAGE_BYTES];   // P2: de-stuffed bytes awaiting a flush
   };
 };
 
@@ -260,6 +266,32 @@ FFCV_DEV uint32_t slow_entry(const TB &T, uint32_t acmask, int slot, uint32_t lo
   return make_entry((acmask >> slot) & 1, len, sym);
 }
 
+// Two AC symbols per first-level lookup.  When a first-level AC entry's
+// symbol (code + extra bits, t1 bits) is not EOB and the next symbol's code
+// and extra bits also fit in the first-level window, the entry carries both:
+//   [0:5) total bits  [5:9) size1  [9:16) z advance of both (clamped 127)
+//   [16:20) t1  [20:24) size2  [24:29) z advance of the first (1..16)
+// A single entry has bits 16.. zero.  A pair never crosses a block end:
+// the decoder takes only the first symbol when it alone reaches z = 64
+// (bits 24.. give its advance, 16.. its bits).  The symbol sequence and
+// every bit position are the same as decoding one symbol per step.
+template <class TB>
+FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, uint32_t look, uint32_t e1) {
+  const int t1 = (int)(e1 & 31), size1 = (int)(e1 >> 5) & 15, zinc1 = (int)(e1 >> 9);
+  if (zinc1 > 16 || t1 >= bits) return e1;  // EOB, or no room for a second code
+  const uint32_t look2 = (look << t1) & 0xffffu;
+  const int room = bits - t1;
+  int len = 1;
+  for (int l = 1; l < 16; l++) len += look2 >= T.lim[slot][l];
+  if (len > room || look2 >= T.lim[slot][len]) return e1;
+  const int sym = T.vals[slot][(T.valoff[slot][len] + (int)(look2 >> (16 - len))) & 0xff];
+  const uint32_t e2 = make_entry(true, len, sym);
+  const int t2 = (int)(e2 & 31), size2 = (int)(e2 >> 5) & 15, zinc2 = (int)(e2 >> 9);
+  if (t2 > room) return e1;
+  return (uint32_t)(t1 + t2) | ((uint32_t)size1 << 5) | ((uint32_t)min(zinc1 + zinc2, 127) << 9) |
+         ((uint32_t)t1 << 16) | ((uint32_t)size2 << 20) | ((uint32_t)zinc1 << 24);
+}
+
 // inf = sinfo of the table: LUT base | bits << 16 | slot << 20 | second-
 // level set << 23.  A slot without a first-level LUT (bits 0) points at a
 // reserved zero word.
@@ -325,10 +357,12 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
     j += adv ? 1 : 0;
     ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
-    const int nbits = hit ? 0 : (int)(e & 31);
+    const int zi1 = (int)(e >> 24);  // pair entry: the first symbol's advance
+    const bool one = zi1 != 0 && z + zi1 >= 64;  // the first symbol ends the block
+    const int nbits = hit ? 0 : (one ? (int)(e >> 16) & 15 : (int)(e & 31));
     br.consume(nbits);
     pos += nbits;
-    z += hit ? 0 : (int)(e >> 9);
+    z += hit ? 0 : (one ? zi1 : (int)(e >> 9) & 127);
     const bool bend = z >= 64;
     z = bend ? 0 : z;
     ph = bend ? nph : ph;
@@ -392,14 +426,22 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecSta
     const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
     const bool isblk = z == 0;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
-    const int nbits = (int)(e & 31), size = (int)(e >> 5) & 15, zinc = (int)(e >> 9);
-    const int raw = (int)((br.acc << (nbits - size)) >> 1 >> (63 - size));
+    const int tot = (int)(e & 31), size = (int)(e >> 5) & 15, zi1 = (int)(e >> 24);
+    const bool pair = zi1 != 0, two = pair && z + zi1 < 64;  // see make_pair
+    const int t1 = pair ? (int)(e >> 16) & 15 : tot;
+    const int zinc = pair ? zi1 : (int)(e >> 9) & 127;
+    const int nbits = two ? tot : t1, zadd = two ? (int)(e >> 9) & 127 : zinc;
+    const int size2 = two ? (int)(e >> 20) & 15 : 0;
+    const int raw = (int)((br.acc << (t1 - size)) >> 1 >> (63 - size));
+    const int raw2 = (int)((br.acc << (tot - size2)) >> 1 >> (63 - size2));
     const int v = size ? huff_extend(raw, size) : 0;
+    const int v2 = size2 ? huff_extend(raw2, size2) : 0;
     br.consume(nbits);
     pos += nbits;
     int16_t *dst = isblk ? dcd + blk : coef + boff + min(z + zinc - 1, 63);
     if (isblk || (size && inwin)) *dst = (int16_t)v;
-    z += zinc;
+    if (size2 && inwin) coef[boff + min(z + zadd - 1, 63)] = (int16_t)v2;
+    z += zadd;
     const bool bend = z >= 64;
     // the next block: (blk + 1, nph, mx', my')
     const bool wrap = nph == 0;
@@ -760,9 +802,9 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
         }
       }
       // first-level LUT space from the pool, in slot order (AC slots first)
-      uint32_t used = 0, nset = 0;
+      uint32_t used = 0, nset = 0, nac = 0;
       for (int q = 0; q < S.nslots; q++) {
-        uint32_t bits = S.slot_tab[q] >= 4 ? FB_AC : FB_DC;
+        uint32_t bits = S.slot_tab[q] >= 4 ? (nac++ ? FB_AC2 : FB_AC) : FB_DC;
         if (used + (1u << bits) > LUT_POOL - 1 || nset == NLUTSLOT) bits = 0;  // canonical decode only
         S.sinfo[q] = (bits ? used : (uint32_t)(LUT_POOL - 1)) | (bits << 16) | ((uint32_t)q << 20) |
                      ((bits ? nset : 0u) << 23);
@@ -950,7 +992,8 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
           e = (uint32_t)(n + 1) << 5;
         }
       }
-      T.lut[(inf & 0xffff) + v] = (uint16_t)e;
+      if (ac && e) e = make_pair(T, s, bits, look, e);
+      T.lut[(inf & 0xffff) + v] = e;
     }
   }
   bar();

@@ -239,6 +239,42 @@ int main(int argc, char **argv) {
     st[dlen++] = d[q];
   }
   tbits = dlen * 8;
+  if (heur == 8) {  // multi-symbol lookup: steps along the true trajectory when one
+                    // lookup of PB bits resolves every whole symbol (code + extra
+                    // bits) inside it, up to MS symbols, never past a block end
+    int PB = getenv("SIM_PAIRB") ? atoi(getenv("SIM_PAIRB")) : 11;
+    int MS = getenv("SIM_MS") ? atoi(getenv("SIM_MS")) : 2;
+    int DCP = getenv("SIM_PAIRDC") ? atoi(getenv("SIM_PAIRDC")) : 0;
+    uint32_t pos = 0;
+    int z = 0, ph = 0;
+    long nsym = 0, nstep = 0;
+    while (pos < tbits) {
+      nstep++;
+      uint32_t p0 = pos;
+      int k = 0;
+      for (;;) {
+        int len, bad, ti = z == 0 ? ph_dc[ph] : ph_ac[ph];
+        int v = sym(ti, pos, &len, &bad);
+        int sz = z == 0 ? v : (v & 15), r = z == 0 ? 0 : v >> 4;
+        int dc = z == 0;
+        if (k > 0 && (pos + len + sz - p0 > (uint32_t)PB || (dc && !DCP))) break;
+        pos += len + sz;
+        nsym++;
+        k++;
+        int zac = sz ? z + r + 1 : (r == 15 ? z + 16 : 64);
+        z = z == 0 ? 1 : zac;
+        if (z >= 64) {
+          z = 0;
+          ph = (ph + 1) % bpm;
+          break;
+        }
+        if (k >= MS || pos >= tbits) break;
+        if (dc && !DCP) break;
+      }
+    }
+    printf("symbols %ld steps %ld (%.3f steps/symbol) PB %d MS %d DCP %d\n", nsym, nstep, (double)nstep / nsym, PB, MS, DCP);
+    return 0;
+  }
   if (heur == 9) {  // sync-distance statistics from random starts
     int8_t *tph = malloc(tbits + 64);
     memset(tph, -1, tbits + 64);

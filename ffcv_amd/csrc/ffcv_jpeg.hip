@@ -65,9 +65,9 @@
 #define FB_AC 11        // first-level bits, the scan's first AC table (luma)
 #define FB_AC2 10       // first-level bits, further AC tables (chroma)
 #define FB_DC 8         // first-level bits, DC tables
-// first-level LUT words shared by the slots (+ the zero word): one table of
+// first-level LUT words shared by the slots (+ two zero words): one table of
 // each AC size and two DC tables, the 4:2:0 / 4:2:2 / 4:4:4 norm
-#define LUT_POOL ((1 << FB_AC) + (1 << FB_AC2) + 2 * (1 << FB_DC) + 1)
+#define LUT_POOL ((1 << FB_AC) + (1 << FB_AC2) + 2 * (1 << FB_DC) + 2)
 #define SUBB 5          // second-level bits
 #define NSUB 8          // second-level tables per slot
 #define NSLOT 6         // Huffman tables a scan can reference (3 DC + 3 AC)
@@ -140,7 +140,7 @@ struct JShared {
   // slot numbers packed 3 bits per phase; per slot LUT base and bits
   int nslots;
   int slot_tab[NSLOT];  // class * 4 + id
-  uint32_t sinfo[NSLOT];  // base | bits << 16 | slot << 20 | second-level set << 23
+  uint32_t sinfo[NSLOT];  // see SI_* below
   uint32_t dinf[10], ainf[10];  // sinfo of each block-in-MCU's DC / AC table
   uint32_t dcpack, acpack, acmask;
   uint32_t scan_off;
@@ -199,21 +199,23 @@ __constant__ int32_t c_aanscales[64] = {
 // reader holds 33..64 valid bits plus the next word, loaded right after a
 // refill and consumed at the following one (~5 symbols later), so a symbol
 // (code <= 16 bits + <= 15 extra bits) never waits on memory.
+typedef const __attribute__((address_space(1))) uint8_t gbytes_t;  // global memory
 struct BitReader {
-  const uint32_t *w;
+  gbytes_t *w;
   uint64_t acc;
   int nb;
-  uint32_t wi;
+  uint32_t wo;   // byte offset of the word in nxt (32-bit: scalar base + vector offset loads)
   uint32_t nxt;  // raw (little-endian) next word: swapped only when used, so
                  // its load is waited for at the next refill, not here
+  FFCV_DEV uint32_t word(uint32_t off) const { return *(const __attribute__((address_space(1))) uint32_t *)(w + off); }
   FFCV_DEV void init(const uint32_t *words, uint32_t p) {
-    w = words;
-    wi = p >> 5;
-    uint32_t w0 = __builtin_bswap32(w[wi]), w1 = __builtin_bswap32(w[wi + 1]);
-    nxt = w[wi + 2];
+    w = (gbytes_t *)words;
+    wo = (p >> 5) * 4;
+    uint32_t w0 = __builtin_bswap32(word(wo)), w1 = __builtin_bswap32(word(wo + 4));
+    wo += 8;
+    nxt = word(wo);
     acc = (((uint64_t)w0 << 32) | (uint64_t)w1) << (p & 31);
     nb = 64 - (int)(p & 31);
-    wi += 2;
   }
   FFCV_DEV void consume(int n) {
     acc <<= n;
@@ -221,12 +223,21 @@ struct BitReader {
     if (nb <= 32) {
       acc |= (uint64_t)__builtin_bswap32(nxt) << (32 - nb);
       nb += 32;
-      nxt = w[++wi];
+      wo += 4;
+      nxt = word(wo);
     }
   }
 };
 
 FFCV_DEV int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(0xFFFFFFFFu << s) + 1 : x; }
+
+// Loop-iteration counters for tools/jpeg_phases.py: a build with
+// -DFFCV_K1_DIAG only (they cost two instructions per decode step).
+#ifdef FFCV_K1_DIAG
+#define K1_DIAG(x) x
+#else
+#define K1_DIAG(x)
+#endif
 
 struct DecState {
   uint32_t pos;
@@ -270,11 +281,13 @@ FFCV_DEV uint32_t slow_entry(const TB &T, uint32_t acmask, int slot, uint32_t lo
 // symbol (code + extra bits, t1 bits) is not EOB and the next symbol's code
 // and extra bits also fit in the first-level window, the entry carries both:
 //   [0:5) total bits  [5:9) size1  [9:16) z advance of both (clamped 127)
-//   [16:20) t1  [20:24) size2  [24:29) z advance of the first (1..16)
+//   [16:21) t1  [21:25) size2  [25:32) z advance of the first (1..16)
 // A single entry has bits 16.. zero.  A pair never crosses a block end:
-// the decoder takes only the first symbol when it alone reaches z = 64
-// (bits 24.. give its advance, 16.. its bits).  The symbol sequence and
-// every bit position are the same as decoding one symbol per step.
+// the decoder takes only the first symbol when it alone reaches z = 64.
+// Then e >> 16 is the first symbol's entry for the sync pass (bits t1 in
+// [0:5), advance in [9:16)), so both passes select with one shift.  The
+// symbol sequence and every bit position are the same as decoding one
+// symbol per step.
 template <class TB>
 FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, uint32_t look, uint32_t e1) {
   const int t1 = (int)(e1 & 31), size1 = (int)(e1 >> 5) & 15, zinc1 = (int)(e1 >> 9);
@@ -289,19 +302,29 @@ FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, uint32_t look, uint
   const int t2 = (int)(e2 & 31), size2 = (int)(e2 >> 5) & 15, zinc2 = (int)(e2 >> 9);
   if (t2 > room) return e1;
   return (uint32_t)(t1 + t2) | ((uint32_t)size1 << 5) | ((uint32_t)min(zinc1 + zinc2, 127) << 9) |
-         ((uint32_t)t1 << 16) | ((uint32_t)size2 << 20) | ((uint32_t)zinc1 << 24);
+         ((uint32_t)t1 << 16) | ((uint32_t)size2 << 21) | ((uint32_t)zinc1 << 25);
 }
 
-// inf = sinfo of the table: LUT base | bits << 16 | slot << 20 | second-
-// level set << 23.  A slot without a first-level LUT (bits 0) points at a
-// reserved zero word.
+// inf = sinfo of the table: [0:5) 32 - first-level bits, [5:21) LUT byte
+// offset, [21:24) slot, [24:27) second-level set, [27:31) first-level bits.
+// The first-level index is the top bits of the reader's high word, one
+// shift by the low field (the shifter reads 5 bits).  A slot without a
+// first-level LUT (bits 0) has shift 31 onto two reserved zero words.
+FFCV_DEV uint32_t si_pack(uint32_t base, uint32_t bits, uint32_t slot, uint32_t set) {
+  return (bits ? 32 - bits : 31) | (base * 4) << 5 | slot << 21 | set << 24 | bits << 27;
+}
+FFCV_DEV uint32_t si_base(uint32_t inf) { return ((inf >> 5) & 0xffff) >> 2; }
+FFCV_DEV int si_bits(uint32_t inf) { return (int)(inf >> 27) & 15; }
+FFCV_DEV int si_set(uint32_t inf) { return (int)(inf >> 24) & 7; }
+
 template <class TB>
 FFCV_DEV uint32_t decode_entry(const TB &T, uint32_t acmask, uint32_t inf, uint64_t acc) {
-  const uint32_t look = (uint32_t)(acc >> 48);
-  const int bits = (int)((inf >> 16) & 15), slot = (int)((inf >> 20) & 7);
-  uint32_t e = T.lut[(inf & 0xffff) + (look >> (16 - bits))];
+  const uint32_t hi = (uint32_t)(acc >> 32);
+  uint32_t e = *(const uint32_t *)((const uint8_t *)T.lut + ((inf >> 5) & 0xffff) + ((hi >> (inf & 31)) << 2));
   if ((e & 31) == 0) {
-    if (e) e = T.lut2[inf >> 23][(e >> 5) - 1][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
+    const uint32_t look = hi >> 16;
+    const int bits = si_bits(inf), slot = (int)(inf >> 21) & 7;
+    if (e) e = T.lut2[si_set(inf)][(e >> 5) - 1][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
     if ((e & 31) == 0) e = slow_entry(T, acmask, slot, look);
   }
   return e;
@@ -324,10 +347,10 @@ FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 
 // and the canonical fallback: with 64 lanes some lane starts or ends a block
 // on almost every step, so those updates are selects fed by loads issued at
 // the top of the step (next phase's table infos, next old event).
-template <class TB>
+template <bool use_old, class TB>
 FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, DecState st,
                              uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, DecState old_exit,
-                             bool use_old, uint32_t &iters) {
+                             uint32_t &iters) {
   BitReader br;
   br.init(words, st.pos);
   uint32_t pos = st.pos;
@@ -343,26 +366,29 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
   int n = 0;
   bool hit = false;
   while (pos < end_bit && !hit) {
-    iters++;
+    K1_DIAG(iters++);
     const int nph = ph + 1 == bpm ? 0 : ph + 1;
     const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
-    const uint32_t onext = evo[min(j + 1, NEV) * JL];
     const bool isblk = z == 0;
     const uint32_t key = (pos << 4) | (uint32_t)ph;
-    hit = isblk && ocur == key;
+    if constexpr (use_old) {
+      const uint32_t onext = evo[min(j + 1, NEV) * JL];
+      hit = isblk && ocur == key;
+      const bool adv = ocur < key;
+      j += adv ? 1 : 0;
+      ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
+    }
     const bool rec = isblk && !hit;
     evn[(rec ? min(n, NEV) : NEV) * JL] = key;
     n += rec ? 1 : 0;
-    const bool adv = ocur < key;
-    j += adv ? 1 : 0;
-    ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
-    const int zi1 = (int)(e >> 24);  // pair entry: the first symbol's advance
-    const bool one = zi1 != 0 && z + zi1 >= 64;  // the first symbol ends the block
-    const int nbits = hit ? 0 : (one ? (int)(e >> 16) & 15 : (int)(e & 31));
+    // a pair whose first symbol ends the block decodes that symbol alone
+    // (e >> 16: its bits and advance); a hit leaves the loop, its step unused
+    const uint32_t v = z + (int)(e >> 25) >= 64 ? e >> 16 : e;
+    const int nbits = (int)(v & 31);
     br.consume(nbits);
     pos += nbits;
-    z += hit ? 0 : (one ? zi1 : (int)(e >> 9) & 127);
+    z += (int)(v >> 9) & 127;
     const bool bend = z >= 64;
     z = bend ? 0 : z;
     ph = bend ? nph : ph;
@@ -420,18 +446,18 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecSta
   bool inwin;
   locate_block(S.pdesc[ph][0], S.pdesc[ph][1], blk, nblocks, mx, my, boff, inwin);
   while (pos < end_bit && !(z == 0 && blk >= nblocks)) {
-    iters++;
+    K1_DIAG(iters++);
     const int nph = ph + 1 == bpm ? 0 : ph + 1;
     const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
     const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
     const bool isblk = z == 0;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
-    const int tot = (int)(e & 31), size = (int)(e >> 5) & 15, zi1 = (int)(e >> 24);
+    const int tot = (int)(e & 31), size = (int)(e >> 5) & 15, zi1 = (int)(e >> 25);
     const bool pair = zi1 != 0, two = pair && z + zi1 < 64;  // see make_pair
-    const int t1 = pair ? (int)(e >> 16) & 15 : tot;
+    const int t1 = pair ? (int)(e >> 16) & 31 : tot;
     const int zinc = pair ? zi1 : (int)(e >> 9) & 127;
     const int nbits = two ? tot : t1, zadd = two ? (int)(e >> 9) & 127 : zinc;
-    const int size2 = two ? (int)(e >> 20) & 15 : 0;
+    const int size2 = two ? (int)(e >> 21) & 15 : 0;
     const int raw = (int)((br.acc << (t1 - size)) >> 1 >> (63 - size));
     const int raw2 = (int)((br.acc << (tot - size2)) >> 1 >> (63 - size2));
     const int v = size ? huff_extend(raw, size) : 0;
@@ -805,9 +831,8 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
       uint32_t used = 0, nset = 0, nac = 0;
       for (int q = 0; q < S.nslots; q++) {
         uint32_t bits = S.slot_tab[q] >= 4 ? (nac++ ? FB_AC2 : FB_AC) : FB_DC;
-        if (used + (1u << bits) > LUT_POOL - 1 || nset == NLUTSLOT) bits = 0;  // canonical decode only
-        S.sinfo[q] = (bits ? used : (uint32_t)(LUT_POOL - 1)) | (bits << 16) | ((uint32_t)q << 20) |
-                     ((bits ? nset : 0u) << 23);
+        if (used + (1u << bits) > LUT_POOL - 2 || nset == NLUTSLOT) bits = 0;  // canonical decode only
+        S.sinfo[q] = si_pack(bits ? used : (uint32_t)(LUT_POOL - 2), bits, (uint32_t)q, bits ? nset : 0u);
         used += bits ? (1u << bits) : 0u;
         nset += bits ? 1u : 0u;
       }
@@ -966,11 +991,11 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
       T.vals[s2][i] = (uint8_t)v;
     }
   }
-  if (tid == 0) T.lut[LUT_POOL - 1] = 0;  // the zero word of LUT-less slots
+  if (tid < 2) T.lut[LUT_POOL - 2 + tid] = 0;  // the zero words of LUT-less slots
   bar();
   for (int s = 0; s < nslots; s++) {
     const uint32_t inf = R.sinfo[s];
-    const int bits = (int)((inf >> 16) & 15);
+    const int bits = si_bits(inf);
     if (!bits) continue;
     const bool ac = (R.acmask >> s) & 1;
     uint32_t L[FB_AC + 1];
@@ -993,18 +1018,18 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
         }
       }
       if (ac && e) e = make_pair(T, s, bits, look, e);
-      T.lut[(inf & 0xffff) + v] = e;
+      T.lut[si_base(inf) + v] = e;
     }
   }
   bar();
   for (int i = tid; i < NSLOT * NSUB * (1 << SUBB); i += NT) {
     const int s = i / (NSUB << SUBB), n = (i >> SUBB) % NSUB, x = i & ((1 << SUBB) - 1);
     if (s >= nslots || n >= min(T.nsub[s], NSUB)) continue;
-    const int bits = (int)((R.sinfo[s] >> 16) & 15);
+    const int bits = si_bits(R.sinfo[s]);
     const uint32_t look = ((uint32_t)T.sub_prefix[s][n] << (16 - bits)) | ((uint32_t)x << (16 - bits - SUBB));
     int len = 1;
     for (int l = 1; l < 16; l++) len += look >= T.lim[s][l];
-    T.lut2[R.sinfo[s] >> 23][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(T, R.acmask, s, look) : (uint16_t)0;
+    T.lut2[si_set(R.sinfo[s])][n][x] = len <= bits + SUBB ? (uint16_t)slow_entry(T, R.acmask, s, look) : (uint16_t)0;
   }
   bar();
 }
@@ -1029,7 +1054,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   int my_nev = 0, my_cb = 0;
   DecState e = g;
   uint32_t it_lane = 0, it_wave = 0;  // diagnostics: loop iterations (max over lanes per round)
-  if (active) e = sync_range(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, g, false, it_lane);
+  if (active) e = sync_range<false>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, g, it_lane);
   if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
   int rounds = 0;
   for (;;) {
@@ -1048,7 +1073,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
         my_nev = 0;
       } else {
         it_lane = 0;
-        e = sync_range(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, e, true, it_lane);
+        e = sync_range<true>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, e, it_lane);
       }
     }
     if (a.dbg) it_wave += __reduce_max_sync(~0ull, changed ? it_lane : 0u);
@@ -1337,7 +1362,14 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     flush((dlen + STREAM_PAD + 3) & ~3u);
   }
   wsync_mem();
+  // one image per wave: its stream base is wave-uniform (scalar registers,
+  // so the refill loads use the scalar-base + 32-bit offset form)
   const uint32_t *words = (const uint32_t *)gds;
+  if constexpr (JL == JT) {
+    const uint64_t wb = (uint64_t)(uintptr_t)gds;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)wb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(wb >> 32));
+    words = (const uint32_t *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  }
   const uint32_t total_bits = dlen * 8;
 
 

@@ -199,6 +199,16 @@ __constant__ int32_t c_aanscales[64] = {
 // reader holds 33..64 valid bits plus the next word, loaded right after a
 // refill and consumed at the following one (~5 symbols later), so a symbol
 // (code <= 16 bits + <= 15 extra bits) never waits on memory.
+// p as a wave-uniform (scalar-register) pointer: every lane of the wave
+// holds the same value when one image maps to one wave.
+template <class P>
+FFCV_DEV P *wave_uniform(P *p) {
+  if constexpr (JL != JT) return p;
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (P *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 typedef const __attribute__((address_space(1))) uint8_t gbytes_t;  // global memory
 struct BitReader {
   gbytes_t *w;
@@ -229,7 +239,6 @@ struct BitReader {
   }
 };
 
-FFCV_DEV int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(0xFFFFFFFFu << s) + 1 : x; }
 
 // Loop-iteration counters for tools/jpeg_phases.py: a build with
 // -DFFCV_K1_DIAG only (they cost two instructions per decode step).
@@ -423,22 +432,31 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
 // to start (z == 0).  Straight-line like sync_range: the next block's
 // destination and window test are computed from the next phase's
 // descriptor (loaded at the top of the step) and selected at a block end.
-FFCV_DEV void locate_block(const int4 pd0, const int4 pd1, int64_t blk, int64_t nblocks, int mx, int my,
+FFCV_DEV void locate_block(const int4 pd0, const int4 pd1, uint32_t blk, uint32_t nblocks, int mx, int my,
                            uint32_t &boff, bool &inwin) {
   // pd0 = {base block, blocks per MCU row, hs, mx_lo}, pd1 = {mx_hi, my_lo, my_hi, -}
   inwin = blk < nblocks && mx >= pd0.w && mx <= pd1.x && my >= pd1.y && my <= pd1.z;
-  boff = ((uint32_t)pd0.x + (uint32_t)my * (uint32_t)pd0.y + (uint32_t)mx * (uint32_t)pd0.z) * 64u;
+  boff = ((uint32_t)pd0.x + __umul24((uint32_t)my, (uint32_t)pd0.y) + __umul24((uint32_t)mx, (uint32_t)pd0.z)) * 64u;
 }
+
+// jdhuff.c HUFF_EXTEND of the s extra bits at bit offset off of w (from
+// the LSB): branch-free, 0 for s = 0.
+FFCV_DEV int huff_value(uint32_t w, uint32_t off, uint32_t s) {
+  const uint32_t raw = __builtin_amdgcn_ubfe(w, off, s), msb = __builtin_amdgcn_ubfe(w, off + s - 1, 1);
+  return (int)(msb ? raw : raw - ((1u << s) - 1u));
+}
+
+typedef __attribute__((address_space(1))) int16_t gshort_t;  // global memory
 
 template <class TB>
 FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecState st, uint32_t end_bit,
-                          int64_t blk, int16_t *coef, int16_t *dcd, uint32_t &iters) {
+                          uint32_t blk, gshort_t *coef, gshort_t *dcd, uint32_t &iters) {
   BitReader br;
   br.init(words, st.pos);
   uint32_t pos = st.pos;
   int z = st.z, ph = st.ph;
   const int bpm = S.bpm, mcux = S.mcux;
-  const int64_t nblocks = S.nblocks;
+  const uint32_t nblocks = (uint32_t)S.nblocks;
   uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
   int m = (int)(blk / bpm);
   int my = m / mcux, mx = m - my * mcux;
@@ -452,21 +470,25 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecSta
     const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
     const bool isblk = z == 0;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
-    const int tot = (int)(e & 31), size = (int)(e >> 5) & 15, zi1 = (int)(e >> 25);
-    const bool pair = zi1 != 0, two = pair && z + zi1 < 64;  // see make_pair
-    const int t1 = pair ? (int)(e >> 16) & 31 : tot;
-    const int zinc = pair ? zi1 : (int)(e >> 9) & 127;
-    const int nbits = two ? tot : t1, zadd = two ? (int)(e >> 9) & 127 : zinc;
-    const int size2 = two ? (int)(e >> 21) & 15 : 0;
-    const int raw = (int)((br.acc << (t1 - size)) >> 1 >> (63 - size));
-    const int raw2 = (int)((br.acc << (tot - size2)) >> 1 >> (63 - size2));
-    const int v = size ? huff_extend(raw, size) : 0;
-    const int v2 = size2 ? huff_extend(raw2, size2) : 0;
+    // see make_pair: vs = this step's bits and z advance
+    const int zi1 = (int)(e >> 25);
+    const bool one = z + zi1 >= 64, pair = zi1 != 0;
+    const uint32_t vs = one ? e >> 16 : e;
+    const int nbits = (int)(vs & 31), zadd = (int)(vs >> 9) & 127;
+    const int t1 = pair ? (int)(e >> 16) & 31 : nbits, zinc = pair ? zi1 : zadd;
+    const uint32_t size = (e >> 5) & 15, size2 = pair && !one ? (e >> 21) & 15 : 0u;
+    // the extra bits sit in the reader's high word (t1, nbits <= 31)
+    const uint32_t hi = (uint32_t)(br.acc >> 32);
+    const int v = huff_value(hi, 32 - t1, size), v2 = huff_value(hi, 32 - nbits, size2);
     br.consume(nbits);
     pos += nbits;
-    int16_t *dst = isblk ? dcd + blk : coef + boff + min(z + zinc - 1, 63);
-    if (isblk || (size && inwin)) *dst = (int16_t)v;
-    if (size2 && inwin) coef[boff + min(z + zadd - 1, 63)] = (int16_t)v2;
+    // (32-bit byte offsets from the scalar bases)
+    auto st16 = [](gshort_t *base, uint32_t i, int x) {
+      *(gshort_t *)((__attribute__((address_space(1))) uint8_t *)base + (i << 1)) = (int16_t)x;
+    };
+    if (isblk) st16(dcd, blk, v);
+    else if (size && inwin) st16(coef, boff + (uint32_t)min(z + zinc - 1, 63), v);
+    if (size2 && inwin) st16(coef, boff + (uint32_t)min(z + zadd - 1, 63), v2);
     z += zadd;
     const bool bend = z >= 64;
     // the next block: (blk + 1, nph, mx', my')
@@ -1100,7 +1122,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   uint32_t it_lane2 = 0;
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur >= 0) write_range(S, T, words, g, my_end, cur, coef, dcd, it_lane2);
+    if (cur >= 0) write_range(S, T, words, g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef), wave_uniform((gshort_t *)dcd), it_lane2);
   }
   if (a.dbg) {
     const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
@@ -1364,12 +1386,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   wsync_mem();
   // one image per wave: its stream base is wave-uniform (scalar registers,
   // so the refill loads use the scalar-base + 32-bit offset form)
-  const uint32_t *words = (const uint32_t *)gds;
-  if constexpr (JL == JT) {
-    const uint64_t wb = (uint64_t)(uintptr_t)gds;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)wb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(wb >> 32));
-    words = (const uint32_t *)(uintptr_t)(((uint64_t)hi << 32) | lo);
-  }
+  const uint32_t *words = wave_uniform((const uint32_t *)gds);
   const uint32_t total_bits = dlen * 8;
 
 

@@ -397,7 +397,7 @@ FFCV_DEV void resize_linear(const ResizePlan &P, const Src &S, int dx, const Lin
     const int e = dx * 3 + c;
     if (e < P.vec_end) {
       int s0 = sat_s16i(h0 >> 4), s1 = sat_s16i(h1 >> 4);
-      int m0 = (s0 * ly.c0) >> 16, m1 = (s1 * ly.c1) >> 16;
+      int m0 = __mul24(s0, ly.c0) >> 16, m1 = __mul24(s1, ly.c1) >> 16;
       int t = sat_s16i(m0 + m1);
       out[c] = sat_u8i((t + 2) >> 2);
     } else {

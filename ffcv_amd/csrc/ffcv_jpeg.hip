@@ -1538,7 +1538,7 @@ struct GPlane {
 struct TPlane {
   const uint8_t *p;
   int r0, c0, pitch;
-  FFCV_DEV int at(int r, int c) const { return p[(r - r0) * pitch + (c - c0)]; }
+  FFCV_DEV int at(int r, int c) const { return p[__mul24(r - r0, pitch) + (c - c0)]; }  // tiles < 2^24 B
 };
 
 // jdsample.c upsampling of one component at full-resolution sample (y, x),
@@ -1646,7 +1646,7 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
   const uint8_t *p;
   int row0;
   int step;
-  FFCV_DEV int at(int y, int x, int c) const { return p[(y - row0) * step + x * 3 + c]; }
+  FFCV_DEV int at(int y, int x, int c) const { return p[__mul24(y - row0, step) + x * 3 + c]; }
 };
 
 template <int MODE, bool FP16>
@@ -1768,8 +1768,12 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
         // 4:2:0: one thread per chroma sample, its 2x2 pixel quad
         const int R0 = Y0 >> 1, C0 = X0 >> 1, qcols = (X1 >> 1) - C0 + 1;
         const int nq = ((Y1 >> 1) - R0 + 1) * qcols;
+        // i / qcols by a float reciprocal: exact while the quotient's
+        // rounding margin 0.5 / qcols exceeds its float error (qcols and
+        // i / qcols well below 2^11 here)
+        const float rq = 1.0f / (float)qcols;
         for (int i = t; i < nq; i += K2T) {
-          const int qr = i / qcols, R = R0 + qr, C = C0 + (i - qr * qcols);
+          const int qr = (int)(((float)i + 0.5f) * rq), R = R0 + qr, C = C0 + (i - __mul24(qr, qcols));
           int cb[4], cr[4];
           upsample_quad_h2v2(tp[1], G.cw[1], G.ch[1], R, C, cb);
           upsample_quad_h2v2(tp[2], G.cw[2], G.ch[2], R, C, cr);
@@ -1779,7 +1783,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
             if (Y < Y0 || Y > Y1 || X < X0 || X > X1) continue;
             int v[3];
             ycc_rgb(tp[0].at(Y, X), cb[u], cr[u], v);
-            rgbx[(Y - Y0) * rw + (X - X0)] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
+            rgbx[__mul24(Y - Y0, rw) + (X - X0)] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
           }
         }
       } else {
@@ -1802,7 +1806,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
       // horizontal pass of crop row r for both columns: sat_s16(h >> 4) per channel
       auto hrow = [&](int r, int H[6]) {
-        const uint32_t *row = rgbx + (r - r0) * rw;
+        const uint32_t *row = rgbx + __mul24(r - r0, rw);
         const uint32_t p0 = row[l0.s], q0 = row[s0b];
         const uint32_t p1 = row[l1.s], q1 = row[s1b];
 #pragma unroll
@@ -1836,7 +1840,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
         int o[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
-          const int m0 = (HA[i] * ly.c0) >> 16, m1 = (HB[i] * ly.c1) >> 16;
+          const int m0 = __mul24(HA[i], ly.c0) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;  // |HA| < 2^15, c <= 2048
           o[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
         }
         if (ep.in_cut(dy, dx0)) {
@@ -2021,7 +2025,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       const int b0[3] = {(int16_t)(Bv.x & 0xffff), (int16_t)(Bv.x >> 16), (int16_t)(Bv.y & 0xffff)};
 #pragma unroll
       for (int c = 0; c < 3; c++) {
-        const int m0 = (a0[c] * ly.c0) >> 16, m1 = (b0[c] * ly.c1) >> 16;
+        const int m0 = __mul24(a0[c], ly.c0) >> 16, m1 = __mul24(b0[c], ly.c1) >> 16;
         v[c] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
       }
     } else if (staged && tabs) {

@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(RRC_THREADS)
       int v[6];
 #pragma unroll
       for (int i = 0; i < 6; i++) {  // VResizeLinearVec_32s8u
-        const int m0 = (HA[i] * ly.c0) >> 16, m1 = (HB[i] * ly.c1) >> 16;
+        const int m0 = __mul24(HA[i], ly.c0) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;  // |HA| < 2^15, c <= 2048
         v[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
       }
       if (ep.in_cut(dy, dx0)) {

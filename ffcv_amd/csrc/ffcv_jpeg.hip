@@ -84,7 +84,10 @@
 #ifndef BAND
 #define BAND 16  // K2 output rows per workgroup
 #endif
-#define K2T 256
+#ifndef K2T
+#define K2T 256  // K2 threads per workgroup
+#endif
+#define K2_COLS 128  // K2 fast path: output column-pair slots (out_w <= 256); K2T / K2_COLS row groups
 #ifndef K2_LDS
 #define K2_LDS 24576  // K2 dynamic LDS: 6 workgroups per CU; bigger bands take the general path (32 KB measured 3% slower)
 #endif
@@ -1718,7 +1721,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
   // words].  Each thread owns one output column pair and walks its half of
   // the band's rows, keeping the two source rows' horizontal sums in
   // registers (resize.cpp HResizeLinear -> VResizeLinearVec_32s8u).
-  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= K2T && !(a.k2flags & 128)) {
+  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && !(a.k2flags & 128)) {
     const int lut_b = FP16 ? 1536 : 0;
     LinTap *rtab = (LinTap *)(lds + lut_b);
     int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
@@ -1795,7 +1798,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
         }
       }
       __syncthreads();
-      const int tx = t % (K2T / 2), sub = t / (K2T / 2);
+      const int tx = t % K2_COLS, sub = t / K2_COLS;
       if (tx >= out_w / 2) return;
       const int dx0 = 2 * tx;
       const LinTap l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
@@ -1817,7 +1820,7 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
           H[3 + c] = sat_s16i((a1 * a1w + b1 * b1w) >> 4);
         }
       };
-      const int half = (BAND + 1) / 2;
+      const int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
       const int ya = oy0 + sub * half, yb = (a.k2flags & 512) ? ya : min(oy1, ya + half);
       int ca = -1, cb = -1;
       int HA[6], HB[6];

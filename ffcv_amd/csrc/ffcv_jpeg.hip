@@ -489,9 +489,13 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecSta
     auto st16 = [](gshort_t *base, uint32_t i, int x) {
       *(gshort_t *)((__attribute__((address_space(1))) uint8_t *)base + (i << 1)) = (int16_t)x;
     };
+#ifndef K1_TIMING_NOSTORE
     if (isblk) st16(dcd, blk, v);
     else if (size && inwin) st16(coef, boff + (uint32_t)min(z + zinc - 1, 63), v);
     if (size2 && inwin) st16(coef, boff + (uint32_t)min(z + zadd - 1, 63), v2);
+#else  // timing only (wrong output): the write pass without its stores
+    if (v == 0x7fffffff && v2 == 0x7fffffff) st16(coef, boff, v);
+#endif
     z += zadd;
     const bool bend = z >= 64;
     // the next block: (blk + 1, nph, mx', my')

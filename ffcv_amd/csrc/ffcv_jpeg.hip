@@ -322,6 +322,47 @@ FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, uint32_t look, uint
 // The first-level index is the top bits of the reader's high word, one
 // shift by the low field (the shifter reads 5 bits).  A slot without a
 // first-level LUT (bits 0) has shift 31 onto two reserved zero words.
+// Write-pass reader: every step issues exactly one buffer load (a lane that
+// does not refill reads out of range: no access, returns 0) and the step
+// then issues exactly three buffer stores (out of range when a lane has
+// nothing to store).  vmcnt counts loads and stores in issue order, so with
+// these static counts the next step waits for its load with vmcnt(3) instead
+// of draining the previous steps' coefficient stores (vmcnt(0), which the
+// conditional global stores forced).
+#define BUF_OOR 0x7ffffff0u  // an offset past every buffer's num_records
+#define BUF_CFG 0x00020000   // raw buffer resource word 3 (gfx9 family)
+struct BufReader {
+  __amdgpu_buffer_rsrc_t rs;
+  uint64_t acc;
+  int nb;
+  uint32_t wo;  // byte offset of the word in nxt
+  uint32_t nxt, ld;
+  bool rp;  // the previous step refilled: its load (ld) is the next word
+  FFCV_DEV uint32_t word(uint32_t off) const { return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0); }
+  FFCV_DEV void init(const uint32_t *words, uint32_t nbytes, uint32_t p) {
+    rs = __builtin_amdgcn_make_buffer_rsrc((void *)words, 0, (int)nbytes, BUF_CFG);
+    wo = (p >> 5) * 4;
+    const uint32_t w0 = __builtin_bswap32(word(wo)), w1 = __builtin_bswap32(word(wo + 4));
+    wo += 8;
+    nxt = word(wo);
+    ld = 0;
+    rp = false;
+    acc = (((uint64_t)w0 << 32) | (uint64_t)w1) << (p & 31);
+    nb = 64 - (int)(p & 31);
+  }
+  FFCV_DEV void begin() { nxt = rp ? ld : nxt; }
+  FFCV_DEV void consume(int n) {
+    acc <<= n;
+    nb -= n;
+    const bool r = nb <= 32;
+    acc |= r ? (uint64_t)__builtin_bswap32(nxt) << (r ? 32 - nb : 0) : 0ull;
+    nb += r ? 32 : 0;
+    wo += r ? 4u : 0u;
+    ld = word(r ? wo : BUF_OOR);
+    rp = r;
+  }
+};
+
 FFCV_DEV uint32_t si_pack(uint32_t base, uint32_t bits, uint32_t slot, uint32_t set) {
   return (bits ? 32 - bits : 31) | (base * 4) << 5 | slot << 21 | set << 24 | bits << 27;
 }
@@ -452,10 +493,13 @@ FFCV_DEV int huff_value(uint32_t w, uint32_t off, uint32_t s) {
 typedef __attribute__((address_space(1))) int16_t gshort_t;  // global memory
 
 template <class TB>
-FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecState st, uint32_t end_bit,
-                          uint32_t blk, gshort_t *coef, gshort_t *dcd, uint32_t &iters) {
-  BitReader br;
-  br.init(words, st.pos);
+FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32_t words_bytes, DecState st,
+                          uint32_t end_bit, uint32_t blk, gshort_t *coef, uint32_t coef_bytes, gshort_t *dcd,
+                          uint32_t dcd_bytes, uint32_t &iters) {
+  BufReader br;
+  br.init(words, words_bytes, st.pos);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)coef, 0, (int)coef_bytes, BUF_CFG);
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc((void *)dcd, 0, (int)dcd_bytes, BUF_CFG);
   uint32_t pos = st.pos;
   int z = st.z, ph = st.ph;
   const int bpm = S.bpm, mcux = S.mcux;
@@ -468,6 +512,7 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecSta
   locate_block(S.pdesc[ph][0], S.pdesc[ph][1], blk, nblocks, mx, my, boff, inwin);
   while (pos < end_bit && !(z == 0 && blk >= nblocks)) {
     K1_DIAG(iters++);
+    br.begin();
     const int nph = ph + 1 == bpm ? 0 : ph + 1;
     const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
     const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
@@ -485,16 +530,15 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, DecSta
     const int v = huff_value(hi, 32 - t1, size), v2 = huff_value(hi, 32 - nbits, size2);
     br.consume(nbits);
     pos += nbits;
-    // (32-bit byte offsets from the scalar bases)
-    auto st16 = [](gshort_t *base, uint32_t i, int x) {
-      *(gshort_t *)((__attribute__((address_space(1))) uint8_t *)base + (i << 1)) = (int16_t)x;
-    };
+    // three stores every step (see BufReader): DC difference, first and
+    // second AC coefficient, each out of range when the lane has none
 #ifndef K1_TIMING_NOSTORE
-    if (isblk) st16(dcd, blk, v);
-    else if (size && inwin) st16(coef, boff + (uint32_t)min(z + zinc - 1, 63), v);
-    if (size2 && inwin) st16(coef, boff + (uint32_t)min(z + zadd - 1, 63), v2);
+    const uint32_t o1 = (boff + (uint32_t)min(z + zinc - 1, 63)) * 2, o2 = (boff + (uint32_t)min(z + zadd - 1, 63)) * 2;
+    __builtin_amdgcn_raw_buffer_store_b16((short)v, drs, isblk ? blk * 2 : BUF_OOR, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, !isblk && size && inwin ? o1 : BUF_OOR, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, size2 && inwin ? o2 : BUF_OOR, 0, 0);
 #else  // timing only (wrong output): the write pass without its stores
-    if (v == 0x7fffffff && v2 == 0x7fffffff) st16(coef, boff, v);
+    if (v == 0x7fffffff && v2 == 0x7fffffff) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, boff, 0, 0);
 #endif
     z += zadd;
     const bool bend = z >= 64;
@@ -1129,7 +1173,9 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   uint32_t it_lane2 = 0;
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-    if (cur >= 0) write_range(S, T, words, g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef), wave_uniform((gshort_t *)dcd), it_lane2);
+    if (cur >= 0)
+      write_range(S, T, words, (uint32_t)a.dstuff_slot, g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef),
+                  (uint32_t)(a.coef_slot * 2), wave_uniform((gshort_t *)dcd), (uint32_t)(a.dcd_slot * 2), it_lane2);
   }
   if (a.dbg) {
     const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);

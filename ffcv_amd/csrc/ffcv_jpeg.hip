@@ -213,6 +213,13 @@ FFCV_DEV P *wave_uniform(P *p) {
 }
 
 typedef const __attribute__((address_space(1))) uint8_t gbytes_t;  // global memory
+// Non-temporal loads of file bytes through the global address space: a
+// generic pointer compiles to flat loads, which count in both vmcnt and
+// lgkmcnt and defeat the compiler's per-load waits (every prefetch waited).
+FFCV_DEV uint8_t gld_u8(const uint8_t *p) { return __builtin_nontemporal_load((gbytes_t *)p); }
+FFCV_DEV uint32_t gld_u32(const uint32_t *p) {
+  return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t *)p);
+}
 struct BitReader {
   gbytes_t *w;
   uint64_t acc;
@@ -767,7 +774,7 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     if (p < HDR_BYTES)
       v = S.hdr[p];
     else
-      v = __builtin_nontemporal_load(src + p);
+      v = gld_u8(src + p);
     return v;
   };
   auto R16 = [&](uint32_t p) -> int { return (B(p) << 8) | B(p + 1); };
@@ -1251,7 +1258,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     for (int r = 0; r < (NW + JL - 1) / JL; r++) {
       const int i = r * JL + t;
       const int b0 = 4 * i - (int)mis;
-      const uint32_t w = i < NW && b0 < (int)nh ? __builtin_nontemporal_load(aw + i) : 0u;
+      const uint32_t w = i < NW && b0 < (int)nh ? gld_u32(aw + i) : 0u;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int idx = b0 + j;
@@ -1286,7 +1293,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       for (int q = 0; q < R.nslots; q++) {
         const uint32_t dr = R.dht_off[R.slot_tab[q]], ds = S.dht_off[S.slot_tab[q]];
         auto hb = [](const JShared &X, const uint8_t *xs, uint32_t p) -> int {
-          return p < HDR_BYTES ? X.hdr[p] : __builtin_nontemporal_load(xs + p);
+          return p < HDR_BYTES ? X.hdr[p] : gld_u8(xs + p);
         };
         int total = 0;
         for (int l = 0; l < 16; l++) total += hb(S, src, ds + l);
@@ -1298,7 +1305,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   if (ref >= 0) {
     const JShared &R = KS.w[ref];
     const uint8_t *rsrc = R.src;
-    auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)__builtin_nontemporal_load(rsrc + p); };
+    auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)gld_u8(rsrc + p); };
     build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
   }
   // (no workgroup barrier below this point: each wave runs on its own)
@@ -1312,7 +1319,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     if (p < HDR_BYTES)
       v = S.hdr[p];
     else
-      v = __builtin_nontemporal_load(src + p);
+      v = gld_u8(src + p);
     return v;
   };
   JTables *gt = (JTables *)(a.gtab + a.gtab_slot * k);
@@ -1356,15 +1363,29 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     // DS_FLUSH steps: a byte store per kept byte would make every prefetch
     // wait behind the stores (gfx9 counts loads and stores in one vmcnt).
     uint32_t fbase = 0;  // stream offset of stage[0] (a multiple of 4)
+    // The flush issues a fixed number of buffer stores per lane (out of range
+    // past the staged bytes), so the prefetched loads issued before it are
+    // waited for with a static vmcnt, not behind a dynamic store count.
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(gds), 0, (int)a.dstuff_slot, BUF_CFG);
+    constexpr int FL_N = (STAGE_BYTES / 4 + JL - 1) / JL;  // stores per lane per flush
     auto flush = [&](uint32_t upto) {  // write stage bytes [fbase, upto), upto % 4 == 0
       wsync_lds();
       const uint32_t nd = (upto - fbase) / 4;
-      for (uint32_t q = t; q < nd; q += JL) ((uint32_t *)gds)[fbase / 4 + q] = ((const uint32_t *)S.stage)[q];
+#pragma unroll
+      for (int f = 0; f < FL_N; f++) {
+        const uint32_t q = (uint32_t)(f * JL + t);
+        const uint32_t v = ((const uint32_t *)S.stage)[min(q, (uint32_t)(STAGE_BYTES / 4 - 1))];
+        __builtin_amdgcn_raw_buffer_store_b32(v, drs, q < nd ? fbase + 4 * q : BUF_OOR, 0, 0);
+      }
       wsync_lds();
     };
     // DS_DEPTH-deep prefetch ring, unrolled so every ring register is consumed in
     // place (a rotating copy would make the compiler wait for all loads)
-    auto ld = [&](uint32_t d) -> uint32_t { return d < ndw ? __builtin_nontemporal_load(aw + d) : 0u; };
+    // segment dwords through a buffer resource: past the segment the load is
+    // out of range and returns 0 with no access, so every step issues its
+    // load unconditionally and the compiler can count vmcnt statically
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc((void *)wave_uniform(aw), 0, (int)(ndw * 4), BUF_CFG);
+    auto ld = [&](uint32_t d) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(srs, d * 4, 0, 0); };
     uint32_t r[DS_DEPTH];
 #pragma unroll
     for (int u = 0; u < DS_DEPTH; u++) r[u] = ld(u * JL + t);
@@ -1374,13 +1395,13 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 #pragma unroll
       for (int u = 0; u < DS_DEPTH; u++) {
         const uint32_t base = base4 + u * JL;
+        const uint32_t w = r[u];
+        r[u] = ld(base + DS_DEPTH * JL + t);  // issued on every step (see srs)
         if (done || base >= ndw) {
           done = true;
           continue;
         }
         const uint32_t di = base + t;
-        const uint32_t w = r[u];
-        r[u] = ld(base + DS_DEPTH * JL + t);
         const uint32_t wprev = lane_prev(w);
         const uint32_t wnext = lane_next(w);
         const uint32_t nfirst = seg_read(r[(u + 1) % DS_DEPTH], 0, sg);  // next step's first dword

@@ -308,14 +308,16 @@ FFCV_DEV uint32_t slow_entry(const TB &T, uint32_t acmask, int slot, uint32_t lo
 // symbol sequence and every bit position are the same as decoding one
 // symbol per step.
 template <class TB>
-FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, uint32_t look, uint32_t e1) {
+FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, const uint32_t *L, uint32_t look, uint32_t e1) {
+  // L[l] = T.lim[slot][l] for l <= FB_AC, in registers
   const int t1 = (int)(e1 & 31), size1 = (int)(e1 >> 5) & 15, zinc1 = (int)(e1 >> 9);
   if (zinc1 > 16 || t1 >= bits) return e1;  // EOB, or no room for a second code
   const uint32_t look2 = (look << t1) & 0xffffu;
   const int room = bits - t1;
-  int len = 1;
-  for (int l = 1; l < 16; l++) len += look2 >= T.lim[slot][l];
-  if (len > room || look2 >= T.lim[slot][len]) return e1;
+  int len = 1;  // the canonical length if it is at most room (limits are non-decreasing)
+#pragma unroll
+  for (int l = 1; l < FB_AC; l++) len += (l < room && look2 >= L[l]) ? 1 : 0;
+  if (look2 >= T.lim[slot][len]) return e1;  // a longer code
   const int sym = T.vals[slot][(T.valoff[slot][len] + (int)(look2 >> (16 - len))) & 0xff];
   const uint32_t e2 = make_entry(true, len, sym);
   const int t2 = (int)(e2 & 31), size2 = (int)(e2 >> 5) & 15, zinc2 = (int)(e2 >> 9);
@@ -766,16 +768,30 @@ struct JpegArgs {
     if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + (slot)] = wall_clock64();  \
   } while (0)
 
-// P0 (one lane): marker walk over the LDS copy of the header bytes.
-FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const ffcv_sample &smp,
-                          const JpegArgs &a, int k, int MODE) {
+// A wave-uniform value in a scalar register (one image per wave).
+FFCV_DEV uint32_t wuni(uint32_t v) {
+  if constexpr (JL == JT) return __builtin_amdgcn_readfirstlane(v);
+  return v;
+}
+
+// P0: marker walk over the LDS copy of the header bytes.  With one image per
+// wave every lane runs it on wave-uniform (scalar) values: each byte read is
+// broadcast to a scalar register, so the walk's branches and arithmetic are
+// scalar instead of one lane under an exec mask.
+FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const ffcv_sample &smp_in,
+                          const JpegArgs &a, int k_in, int MODE) {
+  nbytes = wuni(nbytes);
+  const int k = (int)wuni((uint32_t)k_in);
+  ffcv_sample smp = smp_in;
+  smp.width = wuni(smp_in.width);
+  smp.height = wuni(smp_in.height);
   auto B = [&](uint32_t p) -> int {
     int v;
     if (p < HDR_BYTES)
       v = S.hdr[p];
     else
       v = gld_u8(src + p);
-    return v;
+    return (int)wuni((uint32_t)v);
   };
   auto R16 = [&](uint32_t p) -> int { return (B(p) << 8) | B(p + 1); };
   for (int i = 0; i < 4; i++) S.dqt_ok[i] = 0;
@@ -973,10 +989,15 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     return FFCV_SAMPLE_TOO_LARGE;
   if (MODE == JM_COEF && (uint64_t)S.nblocks > a.max_blocks) return FFCV_SAMPLE_TOO_LARGE;
   if (MODE == JM_RRC) {
-    S.ri = a.crops[4 * k];
-    S.rj = a.crops[4 * k + 1];
-    S.rh = a.crops[4 * k + 2];
-    S.rw = a.crops[4 * k + 3];
+    // vector loads (the fused draws wrote the crop with vector stores in this
+    // kernel; a scalar load at this uniform address could hit a stale K$ line)
+    auto crop = [&](int i) {
+      return (int)wuni((uint32_t)__builtin_nontemporal_load((const __attribute__((address_space(1))) int32_t *)a.crops + 4 * k + i));
+    };
+    S.ri = crop(0);
+    S.rj = crop(1);
+    S.rh = crop(2);
+    S.rw = crop(3);
     if (S.rh <= 0 || S.rw <= 0 || S.ri < 0 || S.rj < 0 || S.ri + S.rh > S.H || S.rj + S.rw > S.W)
       return FFCV_SAMPLE_GEOMETRY;
   } else {
@@ -1097,7 +1118,7 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
           e = (uint32_t)(n + 1) << 5;
         }
       }
-      if (ac && e) e = make_pair(T, s, bits, look, e);
+      if (ac && e) e = make_pair(T, s, bits, L, look, e);
       T.lut[si_base(inf) + v] = e;
     }
   }
@@ -1267,9 +1288,11 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
   }
   wsync_lds();
-  if (t == 0) {
-    S.src = src;
-    S.status = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, src, nbytes, smp, a, k, MODE)) : -1;
+  STAMP(10);
+  if (t == 0) S.src = src;
+  if (JL == JT || t == 0) {  // the whole wave runs the (scalar) parse; see parse_header
+    const int st = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, wave_uniform(src), nbytes, smp, a, k, MODE)) : -1;
+    if (t == 0) S.status = st;
   }
   __syncthreads();
 

@@ -43,6 +43,9 @@ print('phase means (us):')
 for i, n in enumerate(names):
     dt = (d[:, i + 1] - d[:, i]) / 100.0
     print(f'  {n:12s} mean {dt.mean():8.1f}  p50 {np.median(dt):8.1f}  max {dt.max():8.1f}')
+for n, (i0, i1) in (('  header load', (0, 10)), ('  parse+barrier', (10, 1))):
+    dt = (d[:, i1] - d[:, i0]) / 100.0
+    print(f'  {n:12s} mean {dt.mean():8.1f}  p50 {np.median(dt):8.1f}  max {dt.max():8.1f}')
 tot = (d[:, 9] - d[:, 0]) / 100.0
 print('  total        mean', tot.mean(), 'max', tot.max())
 print('span of K1 us', (d[:, 9].max() - d[:, 0].min()) / 100.0)

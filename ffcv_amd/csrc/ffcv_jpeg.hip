@@ -412,7 +412,8 @@ FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 
 template <bool use_old, class TB>
 FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, DecState st,
                              uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, DecState old_exit,
-                             uint32_t &iters) {
+                             int sh, uint32_t &iters) {
+  const int smask = (1 << sh) - 1;  // events: every 2^sh-th block start (slot q = block q << sh)
   BitReader br;
   br.init(words, st.pos);
   uint32_t pos = st.pos;
@@ -441,7 +442,7 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
       ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
     }
     const bool rec = isblk && !hit;
-    evn[(rec ? min(n, NEV) : NEV) * JL] = key;
+    evn[(rec && (n & smask) == 0 ? min(n >> sh, NEV) : NEV) * JL] = key;
     n += rec ? 1 : 0;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
     // a pair whose first symbol ends the block decodes that symbol alone
@@ -457,19 +458,19 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
     dinf = bend ? ndinf : dinf;
     ainf = bend ? nainf : ainf;
   }
-  if (hit) {  // at the previous trajectory's j-th block start
-    int m = n;
-    if (n < NEV) {
-      int keep = min(onev - j, NEV - n);
-      for (int q = 0; q < keep; q++) evn[(n + q) * JL] = evo[(j + q) * JL];
-      m = n + keep;
+  if (hit) {  // at the previous trajectory's event j = its block start j << sh
+    int m = min((n + smask) >> sh, NEV);  // slots written so far
+    if ((n & smask) == 0 && m < NEV) {     // the old events stay on the slot grid: keep them
+      const int keep = min(onev - j, NEV - m);
+      for (int q = 0; q < keep; q++) evn[(m + q) * JL] = evo[(j + q) * JL];
+      m += keep;
     }
-    nev = min(m, NEV);
-    cnt = (uint32_t)n + (cnt - (uint32_t)j);
+    nev = m;
+    cnt = (uint32_t)n + (cnt - ((uint32_t)j << sh));
     cb = nbuf;
     return old_exit;
   }
-  nev = min(n, NEV);
+  nev = min((n + smask) >> sh, NEV);
   cnt = (uint32_t)n;
   cb = nbuf;
   DecState out;
@@ -1155,7 +1156,10 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   int my_nev = 0, my_cb = 0;
   DecState e = g;
   uint32_t it_lane = 0, it_wave = 0;  // diagnostics: loop iterations (max over lanes per round)
-  if (active) e = sync_range<false>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, g, it_lane);
+  // event stride: NEV events spread over a lane's expected block count
+  const uint32_t evq = ((uint32_t)S.nblocks / nthr + NEV) / NEV;
+  const int esh = evq <= 1 ? 0 : 32 - __clz((int)(evq - 1));
+  if (active) e = sync_range<false>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, g, esh, it_lane);
   if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
   int rounds = 0;
   for (;;) {
@@ -1174,7 +1178,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
         my_nev = 0;
       } else {
         it_lane = 0;
-        e = sync_range<true>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, e, it_lane);
+        e = sync_range<true>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, e, esh, it_lane);
       }
     }
     if (a.dbg) it_wave += __reduce_max_sync(~0ull, changed ? it_lane : 0u);

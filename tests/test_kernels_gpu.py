@@ -233,6 +233,43 @@ def test_jpeg_full_decode_matches_libjpeg(hip_lib, oracle):
             assert np.array_equal(want, oracle.ljt_decode(blobs[k]))
 
 
+def test_jpeg_full_decode_large_images(hip_lib, oracle):
+    """Multi-megapixel streams: long lane ranges (many refills per lane, a wide
+    sync-event stride, several sync rounds), every subsampling, greyscale and
+    q100 (long codes through the second-level / canonical tables)."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(33)
+    shapes = [(1200, 1600, '4:2:0', 95), (1500, 2000, '4:2:2', 90), (1024, 1024, '4:4:4', 100),
+              (1601, 999, '4:2:0', 75), (2048, 1536, 'gray', 90)]
+    imgs, blobs = [], []
+    for h, w, sub, q in shapes:
+        img = natural_image(rng, h, w)
+        if sub == 'gray':
+            img = img[:, :, 0].copy()
+            sub = '4:2:0'
+        imgs.append(img)
+        blobs.append(encode_jpeg(img, q, sub))
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    maxh = max(i.shape[0] for i in imgs)
+    maxw = max(i.shape[1] for i in imgs)
+    dec = L.JpegDecoder(B, maxh, maxw, max(len(b) for b in blobs))
+    stride = maxh * maxw * 3
+    out = torch.zeros(B * stride, dtype=torch.uint8, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.decode(d_buf, d_smp, B, out, stride, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    o = out.cpu().numpy()
+    for k in range(B):
+        assert st[k] == 0, (k, st[k])
+        h, w = imgs[k].shape[:2]
+        got = o[k * stride:k * stride + h * w * 3].reshape(h, w, 3)
+        want = oracle.jpeg_decode(blobs[k])
+        assert np.array_equal(got, want), f'sample {k} {imgs[k].shape}'
+
+
 def test_jpeg_coefficients_match_oracle(hip_lib, oracle):
     torch = _torch()
     from ffcv_amd import libffcv as L

@@ -1751,7 +1751,7 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
 };
 
 template <int MODE, bool FP16>
-__global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
+__global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(6))) jpeg_color_resize_kernel(JpegArgs a) {  // 6 WGs per CU (K2_LDS)
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint16_t *s_lut = (uint16_t *)lds;  // 768 entries (FP16)
   const int t = threadIdx.x;
@@ -1792,8 +1792,15 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
     }
     return;
   }
-  if (FP16)
-    for (int i = t; i < 768; i += K2T) s_lut[i] = a.p.lut[i];
+  if (FP16) {  // all loads in flight before the LDS writes
+    constexpr int LU = (768 + K2T - 1) / K2T;
+    uint16_t lv[LU];
+#pragma unroll
+    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? a.p.lut[u * K2T + t] : (uint16_t)0;
+#pragma unroll
+    for (int u = 0; u < LU; u++)
+      if (u * K2T + t < 768) s_lut[u * K2T + t] = lv[u];
+  }
   const int ri = I.ri, rj = I.rj, rh = I.rh, rw = I.rw;
   ResizePlan P = make_plan(rw, rh, out_w, out_h);
   int r0, r1;
@@ -1850,12 +1857,32 @@ __global__ void __launch_bounds__(K2T) jpeg_color_resize_kernel(JpegArgs a) {
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
       if (t < oy1 - oy0) rtab[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
       TPlane tp[3];
+      // tile staging: the first SU dwords per thread of every component are
+      // loaded before any LDS write (one memory round trip, not one per
+      // dword); row = i / wpr by a float reciprocal (exact: i < 2^11 here)
+      constexpr int SU = 4;
+      uint32_t sv[3][SU];
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const int wpr = max(tpitch[c] >> 2, 1), n = (a.k2flags & 1024) ? 0 : trows[c] * (tpitch[c] >> 2);
+        const float rwp = 1.0f / (float)wpr;
+        const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
+#pragma unroll
+        for (int u = 0; u < SU; u++) {
+          const int i = u * K2T + t;
+          const int rr = (int)(((float)i + 0.5f) * rwp), q = i - __mul24(rr, wpr);
+          sv[c][u] = i < n ? *(const uint32_t *)(src + (uint64_t)rr * gp[c].stride + 4 * q) : 0u;
+        }
+      }
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         uint32_t *tl = (uint32_t *)(lds + toff[c]);
-        const int wpr = tpitch[c] >> 2, n = trows[c] * wpr;
+        const int wpr = max(tpitch[c] >> 2, 1), n = (a.k2flags & 1024) ? 0 : trows[c] * (tpitch[c] >> 2);
+#pragma unroll
+        for (int u = 0; u < SU; u++)
+          if (u * K2T + t < n) tl[u * K2T + t] = sv[c][u];
         const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
-        for (int i = t; i < n && !(a.k2flags & 1024); i += K2T) {
+        for (int i = SU * K2T + t; i < n; i += K2T) {  // big tiles
           const int rr = i / wpr, q = i - rr * wpr;
           tl[i] = *(const uint32_t *)(src + (uint64_t)rr * gp[c].stride + 4 * q);
         }

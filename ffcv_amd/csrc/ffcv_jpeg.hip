@@ -164,6 +164,7 @@ struct JShared {
   // as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
   int4 pdesc[10][2];
   int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
+  int qmax[3];  // max |qmul| per component (the IDCT's 32-bit-product test)
   union {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
     uint32_t ev[2][NEV + 1][JL];  // P3: block-start events (pos << 4 | phase), double-buffered
@@ -627,8 +628,10 @@ FFCV_DEV bool seg_any(bool p, int sg) { return seg_ballot(p, sg) != 0; }
 
 // libjpeg post-IDCT range limit: table[x & 1023] (jdmaster.c)
 FFCV_DEV uint8_t idct_rl(int x) {
-  int v = x & 1023;
-  return (uint8_t)(v < 128 ? v + 128 : (v < 512 ? 255 : (v < 896 ? 0 : v - 896)));
+  // table[x & 1023] = x+128 (x & 1023 < 128), 255 (< 512), 0 (< 896), x-896:
+  // with u = (x + 128) & 1023 that is min(u, 255) below 640, else 0
+  const uint32_t u = (uint32_t)(x + 128) & 1023u;
+  return (uint8_t)(u >= 640u ? 0u : min(u, 255u));
 }
 // jidctfst.c MULTIPLY: DESCALE(var * const, CONST_BITS = 8) with a JLONG
 // (64-bit) product.  The 32-bit form is identical whenever the product fits,
@@ -699,20 +702,30 @@ FFCV_DEV void idct_ifast_block(int d[64], uint8_t *out, int stride) {
 // One block: load the zigzag coefficients at cp and zero them, de-zigzag +
 // jidctfst.c DEQUANTIZE (int16 x int16 -> int) with the multipliers qm, and
 // the ifast IDCT into out (stride bytes per row).
-FFCV_DEV void idct_block(int16_t *cp, const int16_t *qm, uint8_t *out, int stride) {
+typedef int16_t s16x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+FFCV_DEV void idct_block(int16_t *cp, const int16_t *qm, int qmax, uint8_t *out, int stride) {
   int16_t zz[64];
   int d[64];
 #pragma unroll
   for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
 #pragma unroll
   for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
-  int mag = 0;
+  // max |coefficient| on packed halves (|-32768| reads as 32768 unsigned);
+  // max|coef| * max|qmul| < 2^14 bounds every dequantised input, so the
+  // 32-bit IDCT products are exact (else the exact 64-bit form runs)
+  u16x2 mu = {0, 0};
 #pragma unroll
-  for (int n = 0; n < 64; n++) {
-    d[n] = (int)zz[kZigzagOfNatural[n]] * (int)qm[n];
-    mag |= d[n] < 0 ? -d[n] : d[n];
+  for (int w = 0; w < 32; w++) {
+    const s16x2 v = *(const s16x2 *)(zz + 2 * w);
+    const s16x2 av = __builtin_elementwise_max(v, (s16x2){0, 0} - v);
+    mu = __builtin_elementwise_max(mu, __builtin_bit_cast(u16x2, av));
   }
-  if (mag < (1 << 14))
+  const int cmax = max((int)mu.x, (int)mu.y);
+#pragma unroll
+  for (int n = 0; n < 64; n++) d[n] = (int)zz[kZigzagOfNatural[n]] * (int)qm[n];
+  if (cmax * qmax < (1 << 14))
     idct_ifast_block<false>(d, out, stride);
   else
     idct_ifast_block<true>(d, out, stride);
@@ -1351,13 +1364,17 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   };
   JTables *gt = (JTables *)(a.gtab + a.gtab_slot * k);
   if (!match) build_tables<JL>(*gt, S, HB, t);
+  if (t < 3) S.qmax[t] = 0;
+  wsync_lds();
   for (int i = t; i < S.ncomp * 64; i += JL) {
     int c = i >> 6, zz = i & 63;
     int tq = S.tq[c];
     uint32_t q = S.dqt_off[tq];
     int qv = S.dqt_prec[tq] ? ((HB(q + 2 * zz) << 8) | HB(q + 2 * zz + 1)) : HB(q + zz);
     int n = c_natural[zz];
-    S.qmul[c][n] = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
+    const int16_t qmv = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
+    S.qmul[c][n] = qmv;
+    atomicMax(&S.qmax[c], qmv < 0 ? -(int)qmv : (int)qmv);
   }
   wsync_lds();  // header bytes are dead from here (P2 stages into the same LDS)
   if (match ? KS.tab.bad : gt->bad) {
@@ -1618,7 +1635,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       const int wbw = S.wx1[c] - S.wx0[c] + 1;
       const int by = S.wy0[c] + j / wbw, bx = S.wx0[c] + j % wbw;
       const int stride = S.bw[c] * 8;
-      idct_block(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64, S.qmul[c],
+      idct_block(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64, S.qmul[c], S.qmax[c],
                  planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
     }
   }

@@ -48,15 +48,41 @@ FFCV_DEV void store_px(void *out, uint64_t idx, const int v[3], const uint16_t *
 }
 
 #define RRC_THREADS 256
+#ifndef RRC_BAND
 #define RRC_BAND 16  // output rows per workgroup
+#endif
+#ifndef RRC_LDS_BYTES
+#define RRC_LDS_BYTES 28672  // source-row stage: 5 workgroups per CU
+#endif
+
+// Crop rows staged in LDS.  LDS row y - r0 holds the 16-byte aligned chunks
+// covering crop row y, so the row's first byte sits at its alignment
+// offset ((lead + (y - r0) * step) & 15) inside the LDS row.
+struct LdsSrc {
+  const uint8_t *p;
+  int pitch, lead, stepmod, r0;
+  FFCV_DEV const uint8_t *row(int y) const {
+    const int r = y - r0;
+    return p + r * pitch + ((lead + r * stepmod) & 15);
+  }
+  FFCV_DEV int at(int y, int x, int c) const { return row(y)[x * 3 + c]; }
+};
 
 // One workgroup per band of RRC_BAND output rows of one image.
+//   Staging: the band's source rows of the crop (band_rows) are copied into
+//   LDS with 16-byte aligned global loads (an aligned chunk holding at least
+//   one byte of the row never crosses a page, so the aligned-down/up edges
+//   are safe), so each source byte is read from HBM once per band and every
+//   tap after that is an LDS read.  Bands whose rows do not fit
+//   RRC_LDS_BYTES read their taps from global memory instead.
 //   Linear fast path (every crop upscaled along some axis, OpenCV's
 //   "area-mode" linear with the SSE2 vertical body on every element): each
-//   thread owns one output column pair and walks the band's rows, keeping
-//   the two source rows' horizontal sums in registers, so the column taps
-//   are computed once per thread and each source row once per column pair.
-//   Otherwise (area downscale, odd widths): the per-pixel restatement.
+//   thread owns four adjacent output columns and walks a slice of the band's
+//   rows, keeping the two source rows' horizontal sums in registers; the four
+//   pixels leave as one 12-byte (u8) or three 8-byte (fp16) stores, so a wave
+//   writes one contiguous run of the output row.
+//   Otherwise (area downscale, copy, widths not a multiple of 4): the
+//   per-pixel restatement, over the staged rows when they fit.
 template <bool FP16>
 __global__ void __launch_bounds__(RRC_THREADS)
     rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
@@ -64,13 +90,13 @@ __global__ void __launch_bounds__(RRC_THREADS)
                    const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
                    void *__restrict__ out) {
   __shared__ uint16_t s_lut[FP16 ? 768 : 1];
+  __shared__ uint4 s_src[RRC_LDS_BYTES / 16];
   __shared__ LinTap s_rt[RRC_BAND];
   const int k = blockIdx.y;
   const int t = threadIdx.x;
   const ffcv_sample s = samples[k];
   if (FP16) {
     for (int i = t; i < 768; i += RRC_THREADS) s_lut[i] = p.lut[i];
-    __syncthreads();
   }
   if (s.mode != 1) return;
   const int oy0 = blockIdx.x * RRC_BAND, oy1 = min(p.out_h, oy0 + RRC_BAND);
@@ -91,35 +117,95 @@ __global__ void __launch_bounds__(RRC_THREADS)
   ep.fill[2] = p.cutout_fill[2];
   char *o = (char *)out + stride * k;
   const int out_w = p.out_w;
-  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * RRC_THREADS) {
-    if (t < oy1 - oy0) s_rt[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
-    __syncthreads();
-    if (t >= out_w / 2) return;
-    const int dx0 = 2 * t;
-    const LinTap l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
-    const LinTap l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
-    // a border tap (src[s] * 2048) as the two-tap form with weights (2048, 0)
-    const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
-    const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
-    auto hrow = [&](int r, int H[6]) {  // resize.cpp HResizeLinear of crop row r: sat_s16(h >> 4)
-      const uint8_t *row = src.p + (uint64_t)r * src.step;
+#ifdef RRC_TIMING_SKIP_AREA
+  if (P.kind != 3) return;
+#endif
+#ifdef RRC_TIMING_SKIP_LINEAR
+  if (P.kind == 3) return;
+#endif
+
+  // ---- stage the band's source rows into LDS
+  int r0, r1;
+  band_rows(P, oy0, oy1, &r0, &r1);
+  const uint64_t row0 = (uint64_t)(uintptr_t)src.p + (uint64_t)r0 * src.step;
+  const int nrows = r1 - r0 + 1;
+  const int nch = (15 + P.sw * 3 + 15) >> 4;  // 16-byte chunks per LDS row (any alignment)
+  const bool staged = nrows * nch * 16 <= RRC_LDS_BYTES;
+  LdsSrc L{(const uint8_t *)s_src, nch * 16, (int)(row0 & 15), (int)(src.step & 15), r0};
+  if (staged) {
+    const int n = nrows * nch;
+    int r = t / nch, c = t - r * nch;
+    const int dr = RRC_THREADS / nch, dc = RRC_THREADS - dr * nch;
+    for (int i0 = 0; i0 < n; i0 += RRC_THREADS * 4) {
+      uint4 v[4];
+      int dst[4];
 #pragma unroll
-      for (int c = 0; c < 3; c++) {
-        const int a0 = row[l0.s * 3 + c], b0 = row[s0b * 3 + c];
-        const int a1 = row[l1.s * 3 + c], b1 = row[s1b * 3 + c];
-        H[c] = sat_s16i((a0 * a0w + b0 * b0w) >> 4);
-        H[3 + c] = sat_s16i((a1 * a1w + b1 * b1w) >> 4);
+      for (int j = 0; j < 4; j++) {  // four loads in flight before their LDS writes
+        dst[j] = -1;
+        v[j] = make_uint4(0, 0, 0, 0);
+        if (i0 + j * RRC_THREADS + t < n) {
+          const uint64_t ra = row0 + (uint64_t)r * src.step;
+          // only chunks holding bytes of this row (none past the dataset's end)
+          if (c < (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4)) {
+            v[j] = *(const uint4 *)(uintptr_t)((ra & ~(uint64_t)15) + 16 * (uint64_t)c);
+            dst[j] = r * nch + c;
+          }
+        }
+        c += dc;
+        r += dr;
+        if (c >= nch) {
+          c -= nch;
+          r++;
+        }
       }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (dst[j] >= 0) s_src[dst[j]] = v[j];
+    }
+  }
+  if (P.kind == 3 && t < oy1 - oy0) s_rt[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+  __syncthreads();
+
+  const bool aligned4 = ((((uintptr_t)out) | stride) & 3) == 0;
+  const int nq = out_w >> 2;  // column quads
+  if (staged && P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 3) == 0 && nq <= RRC_THREADS && aligned4) {
+    // row groups: tpg threads (a power of two >= nq, >= 64) per group, each
+    // group walks its own slice of the band's rows
+    int tpg = 64;
+    while (tpg < nq) tpg <<= 1;
+    const int groups = RRC_THREADS / tpg;
+    const int per = (RRC_BAND + groups - 1) / groups;
+    const int g = t / tpg, q = t - g * tpg;
+    const int gy0 = oy0 + g * per, gy1 = min(oy1, gy0 + per);
+    if (q >= nq || gy0 >= gy1) return;
+    const int dx0 = 4 * q;
+    int xa[4], xb[4], wa[4], wb[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const LinTap l = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + j));
+      // a border tap (src[s] * 2048) as the two-tap form with weights (2048, 0)
+      xa[j] = 3 * l.s;
+      xb[j] = 3 * (l.border ? l.s : l.s + 1);
+      wa[j] = l.border ? 2048 : l.c0;
+      wb[j] = l.border ? 0 : l.c1;
+    }
+    auto hrow = [&](int r, int H[12]) {  // resize.cpp HResizeLinear of crop row r: sat_s16(h >> 4)
+      const uint8_t *row = L.row(r);
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+          H[3 * j + c] = sat_s16i((row[xa[j] + c] * wa[j] + row[xb[j] + c] * wb[j]) >> 4);
     };
     int ca = -1, cb = -1;
-    int HA[6], HB[6];
-    for (int dy = oy0; dy < oy1; dy++) {
+    int HA[12], HB[12];
+    for (int dy = gy0; dy < gy1; dy++) {
       const LinTap ly = s_rt[dy - oy0];
       const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
       if (ra != ca) {
         if (ra == cb) {
 #pragma unroll
-          for (int i = 0; i < 6; i++) HA[i] = HB[i];
+          for (int i = 0; i < 12; i++) HA[i] = HB[i];
         } else {
           hrow(ra, HA);
         }
@@ -129,35 +215,34 @@ __global__ void __launch_bounds__(RRC_THREADS)
         hrow(rb, HB);
         cb = rb;
       }
-      int v[6];
+      int v[12];
 #pragma unroll
-      for (int i = 0; i < 6; i++) {  // VResizeLinearVec_32s8u
+      for (int i = 0; i < 12; i++) {  // VResizeLinearVec_32s8u
         const int m0 = __mul24(HA[i], ly.c0) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;  // |HA| < 2^15, c <= 2048
         v[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
       }
-      if (ep.in_cut(dy, dx0)) {
-        v[0] = ep.fill[0];
-        v[1] = ep.fill[1];
-        v[2] = ep.fill[2];
-      }
-      if (ep.in_cut(dy, dx0 + 1)) {
-        v[3] = ep.fill[0];
-        v[4] = ep.fill[1];
-        v[5] = ep.fill[2];
-      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (ep.in_cut(dy, dx0 + j)) {
+          v[3 * j] = ep.fill[0];
+          v[3 * j + 1] = ep.fill[1];
+          v[3 * j + 2] = ep.fill[2];
+        }
       const uint64_t px = (uint64_t)dy * out_w + dx0;
-      if (FP16) {  // 12-byte group, 4-byte aligned (dx0 even)
-        uint32_t *o32 = (uint32_t *)((uint16_t *)o + px * 3);
-        const uint32_t h0 = s_lut[v[0] * 3], h1 = s_lut[v[1] * 3 + 1], h2 = s_lut[v[2] * 3 + 2];
-        const uint32_t h3 = s_lut[v[3] * 3], h4 = s_lut[v[4] * 3 + 1], h5 = s_lut[v[5] * 3 + 2];
-        o32[0] = h0 | (h1 << 16);
-        o32[1] = h2 | (h3 << 16);
-        o32[2] = h4 | (h5 << 16);
-      } else {
-        uint16_t *o16 = (uint16_t *)((uint8_t *)o + px * 3);
-        o16[0] = (uint16_t)(v[0] | (v[1] << 8));
-        o16[1] = (uint16_t)(v[2] | (v[3] << 8));
-        o16[2] = (uint16_t)(v[4] | (v[5] << 8));
+      if (FP16) {  // 24-byte group, 8-byte aligned (dx0 % 4 == 0)
+        uint32_t h[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) h[i] = s_lut[v[i] * 3 + i % 3];
+        uint2 *o64 = (uint2 *)((uint16_t *)o + px * 3);
+        o64[0] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        o64[1] = make_uint2(h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+        o64[2] = make_uint2(h[8] | (h[9] << 16), h[10] | (h[11] << 16));
+      } else {  // 12-byte group, 4-byte aligned
+        uint3 w;
+        w.x = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        w.y = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
+        w.z = v[8] | (v[9] << 8) | (v[10] << 16) | (v[11] << 24);
+        *(uint3 *)((uint8_t *)o + px * 3) = w;
       }
     }
     return;
@@ -170,6 +255,8 @@ __global__ void __launch_bounds__(RRC_THREADS)
       v[0] = ep.fill[0];
       v[1] = ep.fill[1];
       v[2] = ep.fill[2];
+    } else if (staged) {
+      resize_pixel(P, L, dy, ep.src_x(dx), v);
     } else {
       resize_pixel(P, src, dy, ep.src_x(dx), v);
     }

@@ -171,14 +171,30 @@ def test_raw_rrc_matches_oracle(hip_lib, oracle):
 
 
 def test_raw_rrc_448_c5(hip_lib, oracle):
+    """C5 shapes through the LDS-staged bands: device draws over 512x512
+    sources (linear and area crops), plus a full-frame area crop, odd-offset
+    crops (unaligned LDS row starts) and a y-downscaling linear crop; u8 with
+    cutout, then flip + cutout + fp16 LUT.  The global-tap fallback (rows
+    wider than the LDS stage) is covered by the 1000-wide sources above."""
     rng = np.random.default_rng(5)
-    imgs = [natural_image(rng, 512, 512) for _ in range(16)]
-    crops, cut, _ = _draw(hip_lib, np.arange(16, dtype=np.uint64), [512] * 16, [512] * 16, 0, 0,
-                          cutout=64, out=(448, 448))
-    u8 = oracle.rrc_batch([(im.reshape(-1), 512, 512, 1) for im in imgs], crops, 448, 448,
-                          cutout_yx=cut, cutout_size=64)
+    B = 48
+    imgs = [natural_image(rng, 512, 512) for _ in range(B)]
+    crops, cut, flips = _draw(hip_lib, np.arange(B, dtype=np.uint64), [512] * B, [512] * B, 0, 0,
+                              cutout=64, out=(448, 448), flip_p=0.5)
+    crops = crops.copy()
+    crops[0] = (0, 0, 512, 512)     # area downscale, every row staged
+    crops[1] = (3, 5, 301, 157)     # odd offsets: unaligned LDS row leads
+    crops[2] = (0, 1, 512, 440)     # y downscale inside the linear path (19 staged rows)
+    crops[3] = (100, 7, 50, 505)    # wide, short
+    u8 = oracle.rrc_batch([(im.reshape(-1), 512, 512, 1) for im in imgs], crops, 448, 448)
     got = _run_raw_rrc(hip_lib, imgs, crops, (448, 448), cut, 64)
-    assert np.array_equal(got, u8)
+    want = _oracle_post(u8, None, cut, 64)
+    bad = np.argwhere((got != want).reshape(B, -1).any(1)).ravel()
+    assert bad.size == 0, f'samples {bad[:8]} differ; crops {crops[bad[:4]]}'
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    got = _run_raw_rrc(hip_lib, imgs, crops, (448, 448), cut, 64, (124, 116, 103), flips, lut)
+    want = _oracle_post(u8, flips, cut, 64, (124, 116, 103), lut)
+    assert np.array_equal(got.view(np.uint16), want.view(np.uint16))
 
 
 def _jpeg_set(rng, n, max_side=256):

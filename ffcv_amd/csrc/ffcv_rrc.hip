@@ -92,6 +92,7 @@ __global__ void __launch_bounds__(RRC_THREADS)
   __shared__ uint16_t s_lut[FP16 ? 768 : 1];
   __shared__ uint4 s_src[RRC_LDS_BYTES / 16];
   __shared__ LinTap s_rt[RRC_BAND];
+  __shared__ AreaTaps s_at[RRC_BAND];
   const int k = blockIdx.y;
   const int t = threadIdx.x;
   const ffcv_sample s = samples[k];
@@ -164,11 +165,13 @@ __global__ void __launch_bounds__(RRC_THREADS)
     }
   }
   if (P.kind == 3 && t < oy1 - oy0) s_rt[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+  if (P.kind == 2 && t < oy1 - oy0) s_at[t] = area_taps(P.sh, P.scale_y, oy0 + t);
   __syncthreads();
 
   const bool aligned4 = ((((uintptr_t)out) | stride) & 3) == 0;
   const int nq = out_w >> 2;  // column quads
-  if (staged && P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 3) == 0 && nq <= RRC_THREADS && aligned4) {
+  if (staged && (out_w & 3) == 0 && nq <= RRC_THREADS && aligned4 &&
+      ((P.kind == 3 && P.vec_end == 3 * out_w) || P.kind == 2)) {
     // row groups: tpg threads (a power of two >= nq, >= 64) per group, each
     // group walks its own slice of the band's rows
     int tpg = 64;
@@ -179,6 +182,45 @@ __global__ void __launch_bounds__(RRC_THREADS)
     const int gy0 = oy0 + g * per, gy1 = min(oy1, gy0 + per);
     if (q >= nq || gy0 >= gy1) return;
     const int dx0 = 4 * q;
+    // cutout, then one 12-byte (u8) or three 8-byte (fp16) stores
+    auto put = [&](int dy, int v[12]) {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (ep.in_cut(dy, dx0 + j)) {
+          v[3 * j] = ep.fill[0];
+          v[3 * j + 1] = ep.fill[1];
+          v[3 * j + 2] = ep.fill[2];
+        }
+      const uint64_t px = (uint64_t)dy * out_w + dx0;
+      if (FP16) {  // 24-byte group, 8-byte aligned (dx0 % 4 == 0)
+        uint32_t h[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) h[i] = s_lut[v[i] * 3 + i % 3];
+        uint2 *o64 = (uint2 *)((uint16_t *)o + px * 3);
+        o64[0] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        o64[1] = make_uint2(h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+        o64[2] = make_uint2(h[8] | (h[9] << 16), h[10] | (h[11] << 16));
+      } else {  // 12-byte group, 4-byte aligned
+        uint3 w;
+        w.x = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        w.y = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
+        w.z = v[8] | (v[9] << 8) | (v[10] << 16) | (v[11] << 24);
+        *(uint3 *)((uint8_t *)o + px * 3) = w;
+      }
+    };
+    if (P.kind == 2) {  // ResizeArea_Invoker: column taps once per thread, row taps from LDS
+      AreaTaps tx[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) tx[j] = area_taps(P.sw, P.scale_x, ep.src_x(dx0 + j));
+      for (int dy = gy0; dy < gy1; dy++) {
+        const AreaTaps ty = s_at[dy - oy0];
+        int v[12];
+#pragma unroll
+        for (int j = 0; j < 4; j++) resize_area(L, tx[j], ty, v + 3 * j);
+        put(dy, v);
+      }
+      return;
+    }
     int xa[4], xb[4], wa[4], wb[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -221,29 +263,7 @@ __global__ void __launch_bounds__(RRC_THREADS)
         const int m0 = __mul24(HA[i], ly.c0) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;  // |HA| < 2^15, c <= 2048
         v[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
       }
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (ep.in_cut(dy, dx0 + j)) {
-          v[3 * j] = ep.fill[0];
-          v[3 * j + 1] = ep.fill[1];
-          v[3 * j + 2] = ep.fill[2];
-        }
-      const uint64_t px = (uint64_t)dy * out_w + dx0;
-      if (FP16) {  // 24-byte group, 8-byte aligned (dx0 % 4 == 0)
-        uint32_t h[12];
-#pragma unroll
-        for (int i = 0; i < 12; i++) h[i] = s_lut[v[i] * 3 + i % 3];
-        uint2 *o64 = (uint2 *)((uint16_t *)o + px * 3);
-        o64[0] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        o64[1] = make_uint2(h[4] | (h[5] << 16), h[6] | (h[7] << 16));
-        o64[2] = make_uint2(h[8] | (h[9] << 16), h[10] | (h[11] << 16));
-      } else {  // 12-byte group, 4-byte aligned
-        uint3 w;
-        w.x = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
-        w.y = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
-        w.z = v[8] | (v[9] << 8) | (v[10] << 16) | (v[11] << 24);
-        *(uint3 *)((uint8_t *)o + px * 3) = w;
-      }
+      put(dy, v);
     }
     return;
   }

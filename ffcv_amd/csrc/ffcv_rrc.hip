@@ -51,6 +51,9 @@ FFCV_DEV void store_px(void *out, uint64_t idx, const int v[3], const uint16_t *
 #ifndef RRC_BAND
 #define RRC_BAND 16  // output rows per workgroup
 #endif
+#ifndef RRC_STAGE_UNROLL
+#define RRC_STAGE_UNROLL 8  // 16-byte loads in flight per thread while staging
+#endif
 #ifndef RRC_LDS_BYTES
 #define RRC_LDS_BYTES 28672  // source-row stage: 5 workgroups per CU
 #endif
@@ -137,11 +140,11 @@ __global__ void __launch_bounds__(RRC_THREADS)
     const int n = nrows * nch;
     int r = t / nch, c = t - r * nch;
     const int dr = RRC_THREADS / nch, dc = RRC_THREADS - dr * nch;
-    for (int i0 = 0; i0 < n; i0 += RRC_THREADS * 4) {
-      uint4 v[4];
-      int dst[4];
+    for (int i0 = 0; i0 < n; i0 += RRC_THREADS * RRC_STAGE_UNROLL) {
+      uint4 v[RRC_STAGE_UNROLL];
+      int dst[RRC_STAGE_UNROLL];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {  // four loads in flight before their LDS writes
+      for (int j = 0; j < RRC_STAGE_UNROLL; j++) {  // loads in flight before their LDS writes
         dst[j] = -1;
         v[j] = make_uint4(0, 0, 0, 0);
         if (i0 + j * RRC_THREADS + t < n) {
@@ -160,7 +163,7 @@ __global__ void __launch_bounds__(RRC_THREADS)
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; j++)
+      for (int j = 0; j < RRC_STAGE_UNROLL; j++)
         if (dst[j] >= 0) s_src[dst[j]] = v[j];
     }
   }

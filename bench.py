@@ -342,7 +342,11 @@ def main():
                                 '(one decode launch sequence, HIP events on the slot stream)'
                                 if mode == 'jpg' else 'rrc_raw_kernel'),
                      'kernel_ms': round(kern_ms, 4), 'algorithmic_bytes_per_image': round(unit_bytes, 1),
-                     'note': roof_note},
+                     'note': roof_note,
+                     # launches overlap (K in flight), so one launch's duration includes
+                     # GPU time it shares: the whole-job algorithmic rate beside it
+                     'job_achieved': round(value * unit_bytes / 1e9, 2),
+                     'job_frac': round(value * unit_bytes / 1e9 / HBM_PEAK_GBS, 5)},
         'cpu_baseline': None,
     }
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes

@@ -2000,12 +2000,15 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(6))) j
         }
         const uint64_t p0 = (uint64_t)dy * out_w + dx0;
         if (FP16) {
-          uint32_t *o32 = (uint32_t *)((uint16_t *)ob + p0 * 3);  // 12-byte group, 4-byte aligned
           const uint32_t h0 = s_lut[o[0] * 3], h1 = s_lut[o[1] * 3 + 1], h2 = s_lut[o[2] * 3 + 2];
           const uint32_t h3 = s_lut[o[3] * 3], h4 = s_lut[o[4] * 3 + 1], h5 = s_lut[o[5] * 3 + 2];
-          o32[0] = h0 | (h1 << 16);
-          o32[1] = h2 | (h3 << 16);
-          o32[2] = h4 | (h5 << 16);
+          typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));  // 12-byte group, 4-byte aligned
+          u32x3 w;
+          w.x = h0 | (h1 << 16);
+          w.y = h2 | (h3 << 16);
+          w.z = h4 | (h5 << 16);
+          // streaming output: non-temporal (measured +2.7% C3 over plain stores)
+          __builtin_nontemporal_store(w, (u32x3 *)((uint16_t *)ob + p0 * 3));
         } else {
           uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);
           o16[0] = (uint16_t)(o[0] | (o[1] << 8));

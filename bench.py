@@ -311,7 +311,8 @@ def main():
     value = imgs / elapsed
     if mode == 'jpg':
         unit_bytes = mean_bytes + out * out * 3 * (2 if norm else 1)
-        roof_note = 'S_jpeg + 224*224*3*2 (fp16 out) per image (SURVEY 8d C3)'
+        roof_note = (f'S_jpeg + {out}*{out}*3*{2 if norm else 1} ({"fp16" if norm else "u8"} out) '
+                     f'per image (SURVEY 8d {args.config.upper()})')
     else:
         # crop ROI read (E[h*w]/(H*W) measured per batch below) + output write
         crops_np = slots[0]['crops'].cpu().numpy()

@@ -182,10 +182,12 @@ class BatchContext:
                   ch.empty(self.batch_size * 32, dtype=ch.uint8).pin_memory())
             self._staging[f_ix] = st
         host, dev, desc_host = st
-        mm = self.host_state[0]
-        # native multi-threaded gather out of the mmap (ffcv_host_gather)
-        L.host_gather(mm, table['offset'].astype(np.uint64) + np.uint64(self.dataset.data_base),
-                      sizes, offs, host, nthreads=min(8, max(1, B // 32)))
+        # native multi-threaded gather out of the mmap, or out of the process
+        # cache's page slots (os_cache=False), with ffcv_host_gather
+        from ..memory_managers.process_cache import host_source
+        src, src_off = host_source(self.host_state,
+                                   table['offset'].astype(np.uint64) + np.uint64(self.dataset.data_base))
+        L.host_gather(src, src_off, sizes, offs, host, nthreads=min(8, max(1, B // 32)))
         t = table.copy()
         t['offset'] = offs.astype(np.uint64)
         desc_host[:B * 32].copy_(ch.from_numpy(t.view(np.uint8)))

@@ -231,3 +231,30 @@ def test_distinct_epochs_and_determinism(tmpdir_m):
     e1a = next(iter(a))[0].cpu().clone()
     e0b = next(iter(b))[0].cpu().clone()
     assert ch.equal(e0a, e0b) and not ch.equal(e0a, e1a)
+
+
+@pytest.mark.parametrize('mode,n', [('raw', 200), ('jpg', 500)])
+def test_process_cache_pcie_matches_device_cache(tmpdir_m, mode, n):
+    """os_cache=False + device_cache=False (page scheduler, native gather out
+    of the page slots, H2D per batch) gives the HBM-resident OS-cache result
+    bit for bit, on a .beton spanning several 2 MiB pages."""
+    from ffcv_amd.writer import DatasetWriter, MIN_PAGE_SIZE
+    fn = os.path.join(tmpdir_m, f'paged_{mode}.beton')
+    DatasetWriter(fn, {'image': RGBImageField(write_mode=mode, jpeg_quality=95), 'label': IntField()},
+                  page_size=MIN_PAGE_SIZE, num_workers=1).from_indexed_dataset(
+        NaturalDS(n, hw=(120, 160), var=True, seed=11), chunksize=25)
+    mk = lambda **kw: Loader(fn, batch_size=64, order=OrderOption.RANDOM, seed=3, drop_last=False, pipelines={
+        'image': [RandomResizedCropRGBImageDecoder((64, 64)), Cutout(12, (124, 116, 103)), ToTensor(),
+                  ToDevice(ch.device('cuda:0'), non_blocking=True), ToTorchImage(),
+                  NormalizeImage(MEAN, STD, np.float16)],
+        'label': [IntDecoder(), ToTensor(), ToDevice('cuda:0')]}, **kw)  # noqa: E731
+    a = mk(os_cache=True, device_cache=True)
+    b = mk(os_cache=False, device_cache=False)
+    assert len(b.memory_manager.page_to_samples) > 1
+    for epoch in range(2):
+        seen = 0
+        for (ia, la), (ib, lb) in zip(a, b):
+            assert ch.equal(la, lb)
+            assert ch.equal(ia.view(ch.int16), ib.view(ch.int16))
+            seen += len(lb)
+        assert seen == n

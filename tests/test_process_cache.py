@@ -1,0 +1,103 @@
+"""os_cache=False: the process-cache page scheduler
+(ffcv/memory_managers/process_cache/*; reference test intent:
+test_memory_reader.py / test_basic_pipeline.py run with both caches).
+Schedule invariants on random page sets, and Loader output identical to the
+OS-cache Loader on multi-page .beton files (CPU pipelines)."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from ffcv_amd.loader import Loader, OrderOption
+from ffcv_amd.writer import DatasetWriter, MIN_PAGE_SIZE
+from ffcv_amd.fields import RGBImageField, IntField, BytesField
+from ffcv_amd.memory_managers import ProcessCacheManager
+from ffcv_amd.memory_managers.process_cache import compute_schedule, host_source
+from tests.helpers import ConstDS
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_schedule_slots_are_minimal_and_never_shared(seed):
+    rng = np.random.default_rng(seed)
+    nb = int(rng.integers(1, 40))
+    n_pages = int(rng.integers(1, 30))
+    batches = [set(rng.choice(n_pages, size=int(rng.integers(0, 6)), replace=True).tolist())
+               for _ in range(nb)]
+    sch = compute_schedule(batches, prefetch_ahead=3)
+    first = {p: min(b for b in range(nb) if p in batches[b]) for s in batches for p in s}
+    last = {p: max(b for b in range(nb) if p in batches[b]) for p in first}
+    live = lambda b: [p for p in first if max(0, first[p] - 3) <= b <= last[p]]  # noqa: E731
+    assert set(sch.page_to_slot) == set(first)
+    assert sch.num_slots == max([len(live(b)) for b in range(nb)] + [0])
+    for b in range(nb):
+        slots = [sch.page_to_slot[p] for p in live(b)]
+        assert len(slots) == len(set(slots))           # no two live pages share a slot
+        assert set(sch.needed_at[b]) == {p for p in first if first[p] == b}
+        assert all(first[p] - 3 <= b for p in sch.prefetch_at[b])
+    assert sorted(p for q in sch.prefetch_at for p in q) == sorted(first)
+
+
+def test_empty_schedule():
+    sch = compute_schedule([set(), set()])
+    assert sch.num_slots == 0 and sch.page_to_slot == {}
+
+
+class PairDS(ConstDS):
+    def __getitem__(self, index):
+        i, img = super().__getitem__(index)
+        return i, img, np.full(1 + index % 97, index % 251, np.uint8)
+
+
+@pytest.fixture(scope='module')
+def paged_beton():
+    d = tempfile.mkdtemp()
+    fn = os.path.join(d, 'paged.beton')
+    # ~14 MB of samples over 2 MiB pages
+    DatasetWriter(fn, {'index': IntField(), 'value': RGBImageField(write_mode='raw'),
+                       'blob': BytesField()}, page_size=MIN_PAGE_SIZE,
+                  num_workers=1).from_indexed_dataset(PairDS(2000, hw=(48, 48)), chunksize=50)
+    return fn
+
+
+@pytest.mark.parametrize('order', [OrderOption.SEQUENTIAL, OrderOption.RANDOM])
+def test_process_cache_loader_matches_os_cache(paged_beton, order):
+    kw = dict(batch_size=64, order=order, seed=5, device='cpu', drop_last=False)
+    a = Loader(paged_beton, os_cache=True, **kw)
+    b = Loader(paged_beton, os_cache=False, **kw)
+    assert isinstance(b.memory_manager, ProcessCacheManager)
+    assert len(b.memory_manager.page_to_samples) > 4
+    for epoch in range(2):
+        n = 0
+        for (ia, va, ba), (ib, vb, bb) in zip(a, b):
+            assert np.array_equal(ia.numpy(), ib.numpy())
+            assert np.array_equal(va.numpy(), vb.numpy())
+            for i, img in zip(ib.numpy().reshape(-1), vb.numpy()):
+                assert (img == int(i) % 255).all()
+            n += len(ib)
+        assert n == 2000
+
+
+def test_process_cache_reader_and_host_source(paged_beton):
+    loader = Loader(paged_beton, batch_size=100, os_cache=False, device='cpu', order=OrderOption.RANDOM)
+    mm = loader.memory_manager
+    batches = [loader.traversal_order.sample_order(0)[i:i + 100] for i in range(0, 2000, 100)]
+    ctx = mm.schedule_epoch(batches)
+    ctx.__enter__()
+    try:
+        raw = np.memmap(paged_beton, np.uint8, mode='r')
+        read = mm.compile_reader()
+        md = loader.reader.metadata['f2']
+        for b, batch in enumerate(batches):
+            ctx.start_batch(b)
+            ptrs = md['ptr'][batch].astype(np.uint64)
+            src, offs = host_source(ctx.state, ptrs)
+            for sid, p, o in zip(batch, ptrs, offs):
+                n = int(md['size'][sid])
+                want = np.asarray(raw[int(p):int(p) + n])
+                assert np.array_equal(read(p, ctx.state)[:n], want)
+                assert np.array_equal(src[int(o):int(o) + n], want)
+        with pytest.raises(RuntimeError):
+            ctx.start_batch(0)
+    finally:
+        ctx.__exit__(None, None, None)

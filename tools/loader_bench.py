@@ -10,7 +10,7 @@ the bench generator) with ffcv_amd.writer.DatasetWriter, then iterates
         ToTensor(), ToDevice('cuda:0'), ToTorchImage(), NormalizeImage(mean, std, fp16)],
         'label': [IntDecoder(), ToTensor(), ToDevice('cuda:0')]})
 
-in three modes and prints one JSON line per mode:
+in four modes and prints one JSON line per mode:
   * device_cache   : the .beton is copied to HBM once; per batch only indices
                      move (the bench.py workload, seen through the Loader)
   * pcie_in        : device_cache=False: per batch the compressed byte ranges
@@ -18,6 +18,9 @@ in three modes and prints one JSON line per mode:
                      host -> device (hipMemcpyAsync) before decoding
   * pcie_in_out    : as pcie_in, and each decoded fp16 batch is copied back to
                      pinned host memory (the path starts and ends in host memory)
+  * pcie_in_process_cache : as pcie_in with os_cache=False: the page scheduler
+                     preads the batches' .beton pages into a slot pool and
+                     the native gather reads the samples out of the slots
 Images/s is measured over whole epochs after one warm-up epoch.
 """
 import argparse
@@ -40,6 +43,7 @@ def main():
     ap.add_argument('--epochs', type=int, default=2)
     ap.add_argument('--batch', type=int, default=512)
     ap.add_argument('--dir', default=None)
+    ap.add_argument('--modes', default='device_cache,pcie_in,pcie_in_out,pcie_in_process_cache')
     args = ap.parse_args()
 
     import torch
@@ -70,9 +74,10 @@ def main():
         print(f'# wrote {fn} ({os.path.getsize(fn) / 1e6:.1f} MB) in {time.perf_counter() - t0:.1f}s',
               file=sys.stderr)
     dev = torch.device('cuda:0')
-    for mode in ('device_cache', 'pcie_in', 'pcie_in_out'):
+    for mode in args.modes.split(','):
         loader = Loader(fn, batch_size=args.batch, order=OrderOption.RANDOM, seed=0, drop_last=True,
                         device=dev, device_cache=(mode == 'device_cache'),
+                        os_cache=(mode != 'pcie_in_process_cache'),
                         pipelines={'image': [RandomResizedCropRGBImageDecoder((224, 224)),
                                              Cutout(32, (124, 116, 103)), ToTensor(), ToDevice(dev),
                                              ToTorchImage(), NormalizeImage(IMAGENET_MEAN, IMAGENET_STD,

@@ -101,3 +101,21 @@ def test_process_cache_reader_and_host_source(paged_beton):
             ctx.start_batch(0)
     finally:
         ctx.__exit__(None, None, None)
+
+
+def test_quasi_random_order(paged_beton):
+    """test_traversal_orders.py:60-93 intent for QUASI_RANDOM: every epoch
+    is a permutation of the selected indices, epochs differ, the same seed
+    repeats; samples are drawn page-locally (at most 2*bs pages open)."""
+    mk = lambda **kw: Loader(paged_beton, batch_size=50, order=OrderOption.QUASI_RANDOM, seed=9,  # noqa: E731
+                             device='cpu', drop_last=False, os_cache=False, **kw)
+    a, b = mk(), mk()
+    ea = [np.asarray(a.traversal_order.sample_order(e)) for e in range(3)]
+    assert all(np.array_equal(np.sort(e), np.arange(2000)) for e in ea)
+    assert not np.array_equal(ea[0], ea[1])
+    assert np.array_equal(ea[0], np.asarray(b.traversal_order.sample_order(0)))
+    sub = mk(indices=np.arange(0, 2000, 3))
+    got = np.concatenate([ix.numpy().reshape(-1).copy() for ix, _, _ in sub])
+    assert np.array_equal(np.sort(got), np.arange(0, 2000, 3))
+    with pytest.raises(NotImplementedError):
+        Loader(paged_beton, batch_size=50, order=OrderOption.QUASI_RANDOM, device='cpu', distributed=True)

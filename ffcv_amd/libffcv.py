@@ -156,6 +156,17 @@ def _stream(stream):
 
 
 # ----------------------------------------------------------------- wrappers
+def memcpy_h2d_async(dst, src, nbytes: int, stream):
+    """hipMemcpyAsync host -> device on ``stream`` (pinned ``src``): one
+    library call instead of a torch copy dispatch inside a stream context."""
+    _check(lib().ffcv_memcpy_h2d_async(_p(dst), _p(src), int(nbytes), _stream(stream)), 'ffcv_memcpy_h2d_async')
+
+
+def memcpy_d2h_async(dst, src, nbytes: int, stream):
+    """hipMemcpyAsync device -> host on ``stream`` (pinned ``dst``)."""
+    _check(lib().ffcv_memcpy_d2h_async(_p(dst), _p(src), int(nbytes), _stream(stream)), 'ffcv_memcpy_d2h_async')
+
+
 def memcpy(source: np.ndarray, dest: np.ndarray):
     """ffcv/libffcv.py:51-55 memcpy (host plumbing)."""
     lib().my_memcpy(source.ctypes.data, dest.ctypes.data, source.size * source.itemsize)

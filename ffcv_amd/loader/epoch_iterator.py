@@ -164,8 +164,7 @@ class EpochIterator(Thread):
                 runtime.set_current(ctx)
                 ctx.begin_batch(batch_indices, self.epoch, stream)
                 result = self.loader.graph.run(batch_indices, ctx, self.memory_allocations, batch_slot)
-                self._queue_status(batch_slot, ctx, stream)
-                ctx.end_batch()
+                ctx.end_batch(self._queue_status(batch_slot, ctx, stream))
         else:
             runtime.set_current(ctx)
             ctx.begin_batch(batch_indices, self.epoch, None)
@@ -175,17 +174,25 @@ class EpochIterator(Thread):
 
     # ------------------------------------------------- decode status check --
     def _queue_status(self, slot, ctx, stream):
+        """Copy this batch's per-sample status words to pinned host memory
+        and record an event after them; returns that event (None if no
+        status is pending)."""
         if not ctx.pending_status:
             self._status[slot] = None
-            return
+            return None
+        from .. import libffcv as L
         recs = []
         for i, (status, what) in enumerate(ctx.pending_status):
             host = ctx.status_host(i, status)
-            host.copy_(status, non_blocking=True)
+            if status.is_contiguous():
+                L.memcpy_d2h_async(host, status, status.numel() * status.element_size(), stream)
+            else:
+                host.copy_(status, non_blocking=True)
             recs.append((host, what))
         ev = ch.cuda.Event()
         ev.record(stream)
         self._status[slot] = (ev, recs, np.asarray(ctx.batch_indices).copy())
+        return ev
 
     def _check_status(self, slot, wait=False):
         rec = self._status[slot]

@@ -122,13 +122,17 @@ class BatchContext:
         self.pending_status = []
         if self.dataset is not None and self.dataset.device.type == 'cuda':
             B = len(batch_indices)
+            from .. import libffcv as L
             if self._ids_buf is None:
                 self._ids_buf = ch.empty(self.batch_size, dtype=ch.int64, device=self.dataset.device)
                 self._ids_host = ch.empty(self.batch_size, dtype=ch.int64).pin_memory()
+                self._ids_host_np = self._ids_host.numpy()
             self._wait_host_buffers()
-            self._ids_host[:B].copy_(ch.from_numpy(np.asarray(batch_indices, dtype=np.int64)))
-            with ch.cuda.stream(stream):
-                self._ids_buf[:B].copy_(self._ids_host[:B], non_blocking=True)
+            # host-side cost per batch matters here (the Loader's producer
+            # thread runs close to the kernels' rate): a numpy fill of the
+            # pinned ids and one library hipMemcpyAsync on the slot stream
+            self._ids_host_np[:B] = batch_indices
+            L.memcpy_h2d_async(self._ids_buf, self._ids_host, B * 8, stream)
             self.batch_ids = self._ids_buf[:B]
 
     def _wait_host_buffers(self):
@@ -138,10 +142,14 @@ class BatchContext:
             self._h2d_done.synchronize()
             self._h2d_done = None
 
-    def end_batch(self):
+    def end_batch(self, done_event=None):
+        """``done_event``: an event already recorded on the slot stream after
+        all of this batch's work (the status event), reused instead of a new one."""
         if self.stream is not None:
-            self._h2d_done = ch.cuda.Event()
-            self._h2d_done.record(self.stream)
+            if done_event is None:
+                done_event = ch.cuda.Event()
+                done_event.record(self.stream)
+            self._h2d_done = done_event
 
     def status_host(self, i, like):
         buf = self._status_host.get(i)

@@ -180,6 +180,15 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
         )
 
     def _draw_params(self, ss):
+        key = (int(ss.loader_seed), int(ss.epoch))
+        cached = getattr(self, '_dp_cache', None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        p = self._make_draw_params(ss)
+        self._dp_cache = (key, p)
+        return p
+
+    def _make_draw_params(self, ss):
         from .. import libffcv as L
         p = L.DrawParams()
         p.crop_kind = self.crop_kind

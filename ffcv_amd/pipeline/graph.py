@@ -273,8 +273,18 @@ class Graph:
     def run(self, batch_indices, storage_state, memory, slot):
         results = {}
         count = len(batch_indices)
+        # the slot buffer views of one (memory, slot, count) never change:
+        # built once instead of re-sliced every batch (host time per batch
+        # is what bounds the Loader at the kernels' rate)
+        sel = getattr(self, '_sel_cache', None)
+        if sel is None or sel[0] is not memory:
+            sel = self._sel_cache = (memory, {})
+        mems = sel[1].get((slot, count))
+        if mems is None:
+            mems = sel[1][(slot, count)] = {n.id: select_buffer(memory[n.id], slot, count)
+                                            for n in self.exec_nodes}
         for node in self.exec_nodes:
-            mem = select_buffer(memory[node.id], slot, count)
+            mem = mems[node.id]
             pid = self.exec_parent[node.id]
             if pid is None:
                 fix = self.fieldname_to_fix[node.field_name]

@@ -119,3 +119,42 @@ def test_quasi_random_order(paged_beton):
     assert np.array_equal(np.sort(got), np.arange(0, 2000, 3))
     with pytest.raises(NotImplementedError):
         Loader(paged_beton, batch_size=50, order=OrderOption.QUASI_RANDOM, device='cpu', distributed=True)
+
+
+def _dist_worker(rank, world, port, fn, out):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    res = {}
+    for oc in (True, False):
+        loader = Loader(fn, batch_size=64, order=OrderOption.RANDOM, seed=2, device='cpu', drop_last=False,
+                        distributed=True, os_cache=oc)
+        for epoch in range(2):
+            ids, ok = [], True
+            for ix, img, _ in loader:
+                i = ix.numpy().reshape(-1).copy()
+                ok &= bool(all((im == int(j) % 255).all() for j, im in zip(i, img.numpy())))
+                ids.append(i)
+            res[f'oc{int(oc)}_e{epoch}'] = np.concatenate(ids)
+            res[f'ok{int(oc)}_e{epoch}'] = np.array(ok)
+    np.savez(os.path.join(out, f'r{rank}.npz'), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_process_cache_distributed_world2_gloo(paged_beton):
+    """Each rank's shard (perm[rank::world], random.py:13-27) read through the
+    page scheduler equals the OS-cache read; the two shards cover the epoch."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        port = 29700 + os.getpid() % 500
+        mp.spawn(_dist_worker, args=(2, port, paged_beton, d), nprocs=2, join=True)
+        z = [np.load(os.path.join(d, f'r{r}.npz')) for r in range(2)]
+        for epoch in range(2):
+            for r in range(2):
+                assert np.array_equal(z[r][f'oc1_e{epoch}'], z[r][f'oc0_e{epoch}'])
+                assert bool(z[r][f'ok0_e{epoch}']) and bool(z[r][f'ok1_e{epoch}'])
+            both = np.concatenate([z[r][f'oc0_e{epoch}'] for r in range(2)])
+            assert set(both.tolist()) == set(range(2000)) and len(both) == 2000
+        assert not np.array_equal(z[0]['oc0_e0'], z[0]['oc0_e1'])

@@ -54,8 +54,8 @@ WORKLOAD = {
     'c5': 'C5: raw 512x512 RGB .beton, RRC 448 + Cutout(64) u8, batch 256',
 }
 # batches in flight per config on 16 HW queues (A/B, 3 runs each):
-# C3 10 vs 8 +1.5%, C5 4 vs 8 +1%; C2 stays at the C3-tuned 8
-INFLIGHT = {'c3': 10, 'c2': 8, 'c5': 4}
+# C3 10 vs 8 +1.5%, C5 4 vs 8 +1%; C2 (half-size batches) 14 vs 8 +25%, 16 collapses
+INFLIGHT = {'c3': 10, 'c2': 14, 'c5': 4}
 IMAGENET_MEAN = np.array([0.485, 0.456, 0.406]) * 255
 IMAGENET_STD = np.array([0.229, 0.224, 0.225]) * 255
 

@@ -773,6 +773,7 @@ struct JpegArgs {
                 // bit 5 disables the separable linear resize, bit 6 the 4:2:0 quad colour pass,
                 // bit 7 the linear fast path; timing only: bits 8 / 9 / 10 skip the fast
                 // path's colour pass / column walk / tile staging
+  int diag_only;  // host side only: kernels the launch runs (ffcv_jpeg_set_diag)
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -2234,6 +2235,8 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(6))) j
 // ---------------------------------------------------------------- ctx -----
 struct ffcv_jpeg_ctx {
   uint64_t *dbg;
+  int diag_only;    // diagnostics (ffcv_jpeg_set_diag): kernels a launch runs
+  int diag_k2flags; // diagnostics: K2 timing-only flags
   int max_batch;
   uint32_t max_h, max_w;
   uint64_t max_bytes;
@@ -2276,6 +2279,7 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
   }
   ffcv_jpeg_ctx *c = new ffcv_jpeg_ctx();
   c->max_batch = max_batch;
+  c->diag_only = 7;
   c->max_h = max_height;
   c->max_w = max_width;
   c->max_bytes = max_bytes;
@@ -2317,6 +2321,17 @@ int ffcv_jpeg_set_debug(ffcv_jpeg_ctx *c, uint64_t *dbg) {
   return FFCV_OK;
 }
 
+// Diagnostic hook (not in the public header): which kernels a decode launch
+// runs (bit 0 = K1, bit 2 = K2; timing of one kernel re-run on the previous
+// launch's scratch) and K2 timing-only flags.  Set once per context, never
+// read from the environment on the launch path.
+int ffcv_jpeg_set_diag(ffcv_jpeg_ctx *c, int only, int k2flags) {
+  if (!c) return FFCV_EINVAL;
+  c->diag_only = only ? only : 7;
+  c->diag_k2flags = k2flags;
+  return FFCV_OK;
+}
+
 int ffcv_jpeg_destroy(ffcv_jpeg_ctx *c) {
   if (c) free_ctx(c);
   return FFCV_OK;
@@ -2344,8 +2359,8 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.max_h = c->max_h;
   a.max_w = c->max_w;
   a.dbg = c->dbg;
-  const char *f = getenv("FFCV_K2_FLAGS");  // diagnostics only
-  a.k2flags = f ? atoi(f) : 0;
+  a.k2flags = c->diag_k2flags;
+  a.diag_only = c->diag_only;
   return a;
 }
 
@@ -2369,10 +2384,7 @@ static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void
   const bool fp16 = p->lut != nullptr;
   uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
   a.out_stride = p->out_stride ? p->out_stride : dense;
-  // diagnostics only (timing of one kernel re-run on the previous batch's
-  // scratch): FFCV_JPEG_ONLY bit 0 = K1, bit 2 = K2
-  const char *only_s = getenv("FFCV_JPEG_ONLY");
-  const int only = only_s ? atoi(only_s) : 7;
+  const int only = a.diag_only;
   if (only & 1) {
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");

@@ -17,8 +17,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# FFCV_HIP_LIB: diagnostic A/B of an alternative build of the same sources
-LIB_PATH = os.environ.get('FFCV_HIP_LIB') or os.path.join(_HERE, 'libffcv_hip.so')
+LIB_PATH = os.path.join(_HERE, 'libffcv_hip.so')
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -83,6 +82,7 @@ _SIGS = {
     'ffcv_gather_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_uint64]),
     'ffcv_jpeg_create': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64]),
     'ffcv_jpeg_destroy': (c_int, [c_void_p]),
+    'ffcv_jpeg_set_diag': (c_int, [c_void_p, c_int, c_int]),
     'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'ffcv_jpeg_rrc_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
@@ -257,6 +257,11 @@ class JpegDecoder:
         _check(lib().ffcv_jpeg_decode_batch(self.handle, _stream(stream), _p(base), _p(samples),
                                             int(batch), _p(out), int(out_stride), _p(status)),
                'ffcv_jpeg_decode_batch')
+
+    def set_diag(self, only=7, k2flags=0):
+        """Diagnostics: kernels a launch runs (bit 0 K1, bit 2 K2) and K2
+        timing-only flags, fixed on this context (never read per launch)."""
+        _check(lib().ffcv_jpeg_set_diag(self.handle, int(only), int(k2flags)), 'ffcv_jpeg_set_diag')
 
     def coefficients(self, base, samples, batch, out, max_blocks, status, stream=None):
         _check(lib().ffcv_jpeg_coefficients_batch(self.handle, _stream(stream), _p(base),

@@ -1193,10 +1193,25 @@ typedef struct {
   int err;
 } batch_job;
 
+/* Optional external JPEG decoder for the batch driver (bench.py's CPU
+ * baseline): libjpeg-turbo itself through oracle/ljt_harness.c ljt_decode,
+ * with the reference's TurboJPEG settings (ifast IDCT + fancy upsampling,
+ * libffcv.cpp:104-106).  NULL = this file's restatement. */
+typedef int (*orc_ext_decode_fn)(const unsigned char *buf, unsigned long n, unsigned char *out,
+                                 int dct_method, int fancy, int *w, int *h, int *ncomp);
+static orc_ext_decode_fn g_ext_decode;
+
+void orc_set_jpeg_decoder(void *fn) { g_ext_decode = (orc_ext_decode_fn)fn; }
+
 static void run_sample(batch_job *j, int k, uint8_t *tmp) {
   const orc_sample *s = &j->samples[k];
   const uint8_t *img;
-  if (s->mode == 0) {
+  if (s->mode == 0 && g_ext_decode) {
+    int w = 0, h = 0, nc = 0;
+    int rc = g_ext_decode(s->data, s->size, tmp, 1, 1, &w, &h, &nc);
+    if (rc || (uint32_t)w != s->width || (uint32_t)h != s->height) j->err = rc ? rc : -20;
+    img = tmp;
+  } else if (s->mode == 0) {
     int rc = orc_jpeg_decode(s->data, s->size, tmp, 1);
     if (rc) j->err = rc;
     img = tmp;

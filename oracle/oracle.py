@@ -64,6 +64,7 @@ def lib():
                                        ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_int]
+        _lib.orc_set_jpeg_decoder.argtypes = [ctypes.c_void_p]
         _lib.orc_draw_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -240,6 +241,15 @@ def ljt():
             return None
         _ljt = l
     return _ljt
+
+
+def use_libjpeg_turbo(enable=True):
+    """Route rrc_batch's JPEG decode through libjpeg-turbo itself (SIMD,
+    ifast + fancy) instead of the restatement; returns whether it is on."""
+    l = ljt() if enable else None
+    fn = ctypes.cast(l.ljt_decode, ctypes.c_void_p) if l is not None else None
+    lib().orc_set_jpeg_decoder(fn)
+    return l is not None
 
 
 def ljt_decode(data, dct='ifast', fancy=True):

@@ -347,20 +347,37 @@ __global__ void __launch_bounds__(256) cutout_kernel(uint8_t *__restrict__ img, 
   }
 }
 
-// normalize.py:65: output = table[input * 3 + i % 3]; 12 elements (4 RGB
-// pixels) per lane so loads/stores are dword-shaped.
-__global__ void __launch_bounds__(256) normalize_kernel(const uint8_t *__restrict__ in, uint64_t n,
-                                                        const uint16_t *__restrict__ lut,
-                                                        uint16_t *__restrict__ out) {
-  __shared__ uint16_t s_lut[768];
+// normalize.py:64-65: output = table[input * 3 + i % 3] for any table dtype
+// (the cupy kernel is templated on T); T is the element's bit pattern, so
+// one instantiation per element size serves every dtype of that size.  The
+// 768-entry table lives in LDS; 12 elements (4 RGB pixels) per lane, input
+// read as three dwords when 4-byte aligned.
+template <class T>
+__global__ void __launch_bounds__(256) lut_kernel(const uint8_t *__restrict__ in, uint64_t n,
+                                                  const T *__restrict__ lut, T *__restrict__ out) {
+  __shared__ T s_lut[768];
   for (int i = threadIdx.x; i < 768; i += 256) s_lut[i] = lut[i];
   __syncthreads();
-  uint64_t groups = n / 12;
+  const uint64_t groups = n / 12;
+  const bool aligned = ((uintptr_t)in & 3) == 0;
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * 256) {
     const uint8_t *ip = in + g * 12;
-    uint16_t *op = out + g * 12;
+    uint8_t v[12];
+    if (aligned) {
+      const uint32_t *w = (const uint32_t *)ip;
 #pragma unroll
-    for (int e = 0; e < 12; e++) op[e] = s_lut[ip[e] * 3 + (e % 3)];
+      for (int q = 0; q < 3; q++) {
+        uint32_t x = w[q];
+#pragma unroll
+        for (int b = 0; b < 4; b++) v[4 * q + b] = (uint8_t)(x >> (8 * b));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 12; e++) v[e] = ip[e];
+    }
+    T *op = out + g * 12;
+#pragma unroll
+    for (int e = 0; e < 12; e++) op[e] = s_lut[v[e] * 3 + (e % 3)];
   }
   if (blockIdx.x == 0) {
     for (uint64_t i = groups * 12 + threadIdx.x; i < n; i += 256) out[i] = s_lut[in[i] * 3 + (i % 3)];
@@ -466,18 +483,39 @@ int ffcv_cutout_batch(void *stream, uint8_t *images, int batch, int height, int 
   return FFCV_OK;
 }
 
-int ffcv_normalize_batch(void *stream, const uint8_t *in, uint64_t n, const uint16_t *lut, uint16_t *out) {
-  if (!in || !lut || !out) {
-    ffcv::set_error("ffcv_normalize_batch: invalid arguments");
+int ffcv_lut_batch(void *stream, const uint8_t *in, uint64_t n, const void *lut, int elem_bytes, void *out) {
+  if (!in || !lut || !out || !(elem_bytes == 1 || elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8)) {
+    ffcv::set_error("ffcv_lut_batch: invalid arguments (element size %d)", elem_bytes);
     return FFCV_EINVAL;
   }
   if (n == 0) return FFCV_OK;
   uint64_t groups = n / 12 + 1;
   unsigned gx = (unsigned)((groups + 255) / 256);
-  if (gx > 4096) gx = 4096;
-  hipLaunchKernelGGL(normalize_kernel, dim3(gx), dim3(256), 0, ffcv::as_stream(stream), in, n, lut, out);
-  FFCV_LAUNCH_CHECK("normalize_kernel");
+  if (gx > 8192) gx = 8192;
+  hipStream_t s = ffcv::as_stream(stream);
+  switch (elem_bytes) {
+    case 1:
+      hipLaunchKernelGGL(lut_kernel<uint8_t>, dim3(gx), dim3(256), 0, s, in, n, (const uint8_t *)lut, (uint8_t *)out);
+      break;
+    case 2:
+      hipLaunchKernelGGL(lut_kernel<uint16_t>, dim3(gx), dim3(256), 0, s, in, n, (const uint16_t *)lut,
+                         (uint16_t *)out);
+      break;
+    case 4:
+      hipLaunchKernelGGL(lut_kernel<uint32_t>, dim3(gx), dim3(256), 0, s, in, n, (const uint32_t *)lut,
+                         (uint32_t *)out);
+      break;
+    default:
+      hipLaunchKernelGGL(lut_kernel<uint64_t>, dim3(gx), dim3(256), 0, s, in, n, (const uint64_t *)lut,
+                         (uint64_t *)out);
+      break;
+  }
+  FFCV_LAUNCH_CHECK("lut_kernel");
   return FFCV_OK;
+}
+
+int ffcv_normalize_batch(void *stream, const uint8_t *in, uint64_t n, const uint16_t *lut, uint16_t *out) {
+  return ffcv_lut_batch(stream, in, n, lut, 2, out);
 }
 
 int ffcv_flip_batch(void *stream, const uint8_t *in, uint8_t *out, int batch, int height, int width,

@@ -11,6 +11,7 @@ from ..pipeline.allocation_query import AllocationQuery
 
 
 class BytesDecoder(Operation):
+    per_sample = True
 
     def declare_state_and_memory(self, previous_state: State) -> Tuple[State, AllocationQuery]:
         max_size = self.metadata['size'].max()

@@ -75,6 +75,7 @@ class SimpleRGBImageDecoder(Operation):
     Constant-resolution datasets only; reads (and decompresses) images as is.
     """
     device_aware = True
+    per_sample = True
 
     def __init__(self):
         super().__init__()
@@ -179,20 +180,20 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
              AllocationQuery((1,), ch.int32, dev)),  # decode status
         )
 
-    def _draw_params(self, ss):
-        key = (int(ss.loader_seed), int(ss.epoch))
+    def _draw_params(self, ss, out_h, out_w):
+        key = (int(ss.loader_seed), int(ss.epoch), out_h, out_w)
         cached = getattr(self, '_dp_cache', None)
         if cached is not None and cached[0] == key:
             return cached[1]
-        p = self._make_draw_params(ss)
+        p = self._make_draw_params(ss, out_h, out_w)
         self._dp_cache = (key, p)
         return p
 
-    def _make_draw_params(self, ss):
+    def _make_draw_params(self, ss, out_h, out_w):
         from .. import libffcv as L
         p = L.DrawParams()
         p.crop_kind = self.crop_kind
-        p.out_h, p.out_w = int(self.output_size[0]), int(self.output_size[1])
+        p.out_h, p.out_w = out_h, out_w
         if self.crop_kind == 0:
             p.scale[0], p.scale[1] = float(self.scale[0]), float(self.scale[1])
             p.ratio[0], p.ratio[1] = float(self.ratio[0]), float(self.ratio[1])
@@ -208,9 +209,7 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
     def generate_code(self) -> Callable:
         from .. import libffcv as L
         f_ix = self._field_index
-        out_h, out_w = int(self.output_size[0]), int(self.output_size[1])
         rp = L.RRCParams()
-        rp.out_h, rp.out_w = out_h, out_w
         cut = self._fused_cutout
         if cut is not None:
             rp.cutout_size = int(cut.crop_size)
@@ -226,7 +225,11 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
             out, smp, crops, cyx, flips, status = storage
             B = len(batch_indices)
             stream = ss.stream
-            dp = self._draw_params(ss)
+            # the target size is the destination's, like the reference's
+            # resize_crop(..., destination[dst_ix]) (rgb_image.py:207-208):
+            # a new output_size between epochs gets new buffers and is used
+            rp.out_h, rp.out_w = int(out.shape[1]), int(out.shape[2])
+            dp = self._draw_params(ss, rp.out_h, rp.out_w)
             if norm is not None:
                 rp.lut = norm.device_lut(out.device).data_ptr()
             rp.out_stride = out[0].numel() * out.element_size()

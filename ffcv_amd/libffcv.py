@@ -95,6 +95,7 @@ _SIGS = {
     'ffcv_cutout_batch': (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                   c_void_p]),
     'ffcv_normalize_batch': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+    'ffcv_lut_batch': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_int, c_void_p]),
     'ffcv_flip_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                 c_void_p]),
 }
@@ -216,6 +217,13 @@ def cutout_batch(images, yx, crop_size, fill, stream=None):
 def normalize_batch(inp, lut, out, stream=None):
     _check(lib().ffcv_normalize_batch(_stream(stream), _p(inp), int(inp.numel()), _p(lut),
                                       _p(out)), 'ffcv_normalize_batch')
+
+
+def lut_batch(inp, lut, out, stream=None):
+    """out[i] = lut[inp[i]*3 + i%3] for a [256,3] device table of any dtype
+    (element size 1/2/4/8)."""
+    _check(lib().ffcv_lut_batch(_stream(stream), _p(inp), int(inp.numel()), _p(lut),
+                                int(lut.element_size()), _p(out)), 'ffcv_lut_batch')
 
 
 def flip_batch(inp, out, flips, stream=None):

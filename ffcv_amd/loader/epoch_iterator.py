@@ -1,21 +1,38 @@
 """Epoch iterator (ffcv/loader/epoch_iterator.py:33-175).
 
-Same structure as the reference: a background thread builds batches into a
-ring of ``batches_ahead + 2`` slots, each slot owning a HIP stream; a
-bounded queue hands (slot, result) to the consumer, whose ``__next__``
-makes the current stream wait on the slot's stream; an event recorded on the
-consumer stream keeps a slot from being overwritten while still in use.
+Same contract as the reference: a background thread builds batches ahead of
+the training loop into a ring of buffers, each ring entry owning a HIP
+stream; a bounded queue hands them to the consumer, whose ``__next__`` makes
+the current stream wait on the batch's stream; an event recorded on the
+consumer stream keeps a buffer from being overwritten while still in use.
 
-What changed: the stages enqueue HIP kernels on the slot's stream instead of
-running numba loops, so the thread only orchestrates; per-sample decode
-status codes are copied back asynchronously and checked without stalling
-the pipeline (a corrupt or unsupported JPEG raises FFCVError; the reference
-silently returns garbage, rgb_image.py:131,196).
+What changed for MI355X:
+
+* The stages enqueue HIP kernels instead of running numba loops, so the
+  thread only orchestrates.
+* **Launch groups.**  One batch of JPEG decode is 128 entropy workgroups,
+  an eighth of what the GPU holds; the reference's one-batch-per-stream ring
+  therefore needed 10 concurrent streams (and a raised GPU_MAX_HW_QUEUES) to
+  fill the chip.  When every operation of the graph is ``per_sample`` (the
+  north-star pipeline is), ``G`` consecutive batches run through the graph
+  as ONE launch sequence of ``G * batch_size`` samples into one buffer set,
+  and the consumer receives them one batch at a time (views of that set).
+  Three sets rotate (two launches in flight while the consumer reads the
+  third), on three streams, which HIP's default 4 hardware queues hold.
+  Graphs with batch-level operations (mixup, user ops) keep G = 1.
+* Buffer sets are released by the consumer: ``__next__`` records an event on
+  the consumer stream once the previous set's last batch has been handed
+  out; the producer waits (host side) for that release before re-using a
+  set, and the set's stream waits (device side) on the event.
+* Per-sample decode status is copied back asynchronously and checked before
+  the set is reused and at the end of the epoch (a corrupt or unsupported
+  JPEG raises DecodeError; the reference silently returns garbage,
+  rgb_image.py:131,196).
 """
 import os
+import threading
 import time
-from queue import Queue, Full
-from threading import Thread, Event
+from queue import Queue, Full, Empty
 
 import numpy as np
 import torch as ch
@@ -24,70 +41,106 @@ from ..pipeline import runtime
 from ..pipeline.compiler import Compiler
 from ..utils import chunks
 
+# samples per decode launch that fill the GPU (bench.py GROUP: 12 x 512)
+TARGET_LAUNCH_SAMPLES = 6144
+MAX_GROUP = 32
+N_SETS = 3
+
 
 class DecodeError(RuntimeError):
     pass
 
 
-def max_streams():
-    """Slot streams the Loader may use: one hardware queue stays free for the
-    consumer's stream.  10 concurrent batches measured fastest on 16 queues
-    (device_cache Loader 1.92 M vs 1.73 M images/s at 8; bench.py C3 likewise)."""
+def hw_queues():
+    """Hardware queues HIP gives this process: GPU_MAX_HW_QUEUES as it was
+    when the runtime initialised (ffcv never rewrites it), HIP's default 4
+    when unset."""
     try:
-        hwq = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
-        cap = int(os.environ.get('FFCV_LOADER_STREAMS', '10'))  # diagnostic override
+        return max(1, int(os.environ.get('GPU_MAX_HW_QUEUES', '4')))
     except ValueError:
-        hwq, cap = 4, 10
-    return max(1, min(cap, hwq - 1))
+        return 4
 
 
-class EpochIterator(Thread):
+def max_streams():
+    """Producer streams: one hardware queue stays free for the consumer's."""
+    return max(1, hw_queues() - 1)
+
+
+def launch_group(loader, n_batches):
+    """Batches per launch for this loader (1 when the graph mixes samples)."""
+    if loader.batches_per_launch is not None:
+        g = int(loader.batches_per_launch)
+    elif loader.device.type != 'cuda' or not loader.graph.groupable():
+        g = 1
+    else:
+        g = -(-TARGET_LAUNCH_SAMPLES // loader.batch_size)
+    return max(1, min(g, MAX_GROUP, max(1, n_batches)))
+
+
+class EpochIterator(threading.Thread):
     def __init__(self, loader, order):
         super().__init__(daemon=True)
         self.loader = loader
         self.order = order
         self.metadata = loader.reader.metadata
-        self.current_batch_slot = 0
-        batches = list(chunks(order, self.loader.batch_size))
-        self.iter_ixes = iter(batches)
-        self.closed = False
-        self.output_queue = Queue(self.loader.batches_ahead)
-        self.terminate_event = Event()
-        self.memory_context = self.loader.memory_manager.schedule_epoch(batches)
-        self.epoch = loader.next_epoch - 1
-        self.error = None
         self.device = loader.device
         self.is_cuda = self.device.type == 'cuda'
+        self.epoch = loader.next_epoch - 1
+        self.error = None
+        self.closed = False
+        self.terminate_event = threading.Event()
+        bs = loader.batch_size
+        batches = list(chunks(order, bs))
+        self.G = launch_group(loader, len(batches))
+        # groups of G consecutive batches; the last group may be shorter and
+        # its last batch partial (drop_last=False)
+        self.groups = [batches[i:i + self.G] for i in range(0, len(batches), self.G)]
+        self.output_queue = Queue(max(1, loader.batches_ahead))
+        # the page scheduler (os_cache=False) sees one launch as one "batch"
+        self.memory_context = loader.memory_manager.schedule_epoch(
+            [np.concatenate(g) if len(g) else np.zeros(0, np.uint64) for g in self.groups])
+        self.memory_context.__enter__()
+        self.storage_state = self.memory_context.state
         if self.is_cuda:
             self.current_stream = ch.cuda.current_stream(self.device)
-        try:
-            self.memory_context.__enter__()
-        except MemoryError as e:
-            raise e
-        self.storage_state = self.memory_context.state
-        # decode slots: at least batches_ahead + 2 (the reference's ring), and
-        # at least max_streams() so that many batches can be decoding at once
-        # (8 in flight measured fastest on MI355X); batches_ahead still bounds
-        # how far the producer runs ahead of the consumer (the output queue)
-        n_slots = max(self.loader.batches_ahead + 2, max_streams() if self.is_cuda else 0)
-        self.n_slots = n_slots
-        # Slot state lives on the loader across epochs: the device buffers and
-        # the JPEG decoder scratch (hundreds of MB per slot) are allocated
-        # once, not per epoch.  The slots share at most max_streams() HIP
-        # streams (slot % n; two slots on one stream are simply ordered), so
-        # the slot streams plus the consumer's fit the GPU's hardware queues
-        # (GPU_MAX_HW_QUEUES, raised to 16 by ffcv_amd/__init__.py).
-        key = (n_slots, self.loader.batch_size)
+        self.n_sets = N_SETS if self.G > 1 else max(N_SETS, loader.batches_ahead + 2)
+        self._bind_sets()
+        # set release bookkeeping (consumer -> producer)
+        self._cv = threading.Condition()
+        self._released = [True] * self.n_sets      # set may be (re)filled
+        self._release_event = [None] * self.n_sets  # consumer-stream event to wait on
+        self._pending_release = None                # set whose last batch the consumer holds
+        self._status = [None] * self.n_sets
+        self._t_pipeline = 0.0
+        self.start()
+
+    # -------------------------------------------------------------- buffers --
+    def _bind_sets(self):
+        """Per-set device buffers, batch contexts and streams, cached on the
+        loader across epochs while the graph's allocations and the launch
+        shape stay the same (the reference re-allocates every epoch,
+        epoch_iterator.py:65; a resolution change between epochs therefore
+        gets new buffers here too)."""
+        loader = self.loader
+        graph = loader.graph
+        graph.collect_requirements()  # per epoch, like graph.py:356-358
+        cap = self.G * loader.batch_size
+        key = (self.n_sets, cap, graph.allocation_signature())
         cache = getattr(loader, '_slot_cache', None)
         if cache is None or cache['key'] != key:
-            streams = [(ch.cuda.Stream(self.device) if self.is_cuda else None)
-                       for _ in range(min(n_slots, max_streams()))]
+            if cache is not None and self.is_cuda:
+                ch.cuda.synchronize(self.device)  # old buffers may still be read
+            n_streams = min(self.n_sets, max_streams())
+            streams = [(ch.cuda.Stream(self.device) if self.is_cuda else None) for _ in range(n_streams)]
             cache = {'key': key,
-                     'streams': [streams[s % len(streams)] for s in range(n_slots)],
-                     'memory': self.loader.graph.allocate_memory(self.loader.batch_size, n_slots),
-                     'contexts': [runtime.BatchContext(None, loader.device_dataset, loader.seed, s,
-                                                       loader.batch_size) for s in range(n_slots)]}
+                     'streams': [streams[s % n_streams] for s in range(self.n_sets)],
+                     'memory': graph.allocate_memory(cap, self.n_sets),
+                     'contexts': [runtime.BatchContext(None, loader.device_dataset, loader.seed, s, cap)
+                                  for s in range(self.n_sets)]}
             loader._slot_cache = cache
+        else:
+            # same buffers, new node ids (recompile / per-epoch requirements)
+            cache['memory'] = graph.rebind_memory(cache['memory'])
         self.cuda_streams = cache['streams']
         self.memory_allocations = cache['memory']
         self.contexts = cache['contexts']
@@ -99,88 +152,98 @@ class EpochIterator(Thread):
             ev.record(self.current_stream)
             for st in set(self.cuda_streams):
                 st.wait_event(ev)
-        self._status = [None] * n_slots
-        self._t_pipeline = 0.0  # host seconds spent enqueueing batches (FFCV_LOADER_TIMING=1 prints it)
-        self.start()
 
     # ------------------------------------------------------------- thread --
     def run(self):
-        if os.environ.get('FFCV_LOADER_PROFILE'):  # diagnostics: cProfile of the producer thread
-            import cProfile
-            import pstats
-            prof = cProfile.Profile()
-            prof.enable()
-            try:
-                self._run()
-            finally:
-                prof.disable()
-                pstats.Stats(prof).sort_stats('tottime').print_stats(25)
-            return
-        self._run()
-
-    def _run(self):
-        events = [None for _ in self.cuda_streams]
         try:
-            b_ix = 0
             Compiler.set_num_threads(self.loader.num_workers)
-            while True:
-                ixes = next(self.iter_ixes)
-                slot = self.current_batch_slot
-                self.current_batch_slot = (slot + 1) % self.n_slots
+            prev = None
+            for m, group in enumerate(self.groups):
+                s = m % self.n_sets
+                if not self._acquire(s):
+                    return
                 t0 = time.perf_counter()
-                result = self.run_pipeline(b_ix, ixes, slot, events[slot])
+                results = self.run_pipeline(m, group, s)
                 self._t_pipeline += time.perf_counter() - t0
-                to_output = (slot, result)
-                while True:
-                    try:
-                        self.output_queue.put(to_output, block=True, timeout=0.5)
-                        break
-                    except Full:
-                        pass
-                    if self.terminate_event.is_set():
-                        return
-                if self.is_cuda:
-                    just_finished_slot = (slot - self.loader.batches_ahead - 1) % self.n_slots
-                    event = ch.cuda.Event()
-                    event.record(self.current_stream)
-                    events[just_finished_slot] = event
-                b_ix += 1
-        except StopIteration:
+                # hand out the previous launch while this one runs on the GPU
+                if prev is not None and not self._put_group(*prev):
+                    return
+                prev = (s, group, results)
+            if prev is not None and not self._put_group(*prev):
+                return
             if os.environ.get('FFCV_LOADER_TIMING'):
-                print(f'# epoch {self.epoch}: {b_ix} batches, host enqueue {self._t_pipeline * 1e3 / max(1, b_ix):.3f} '
-                      f'ms/batch', flush=True)
-            self.output_queue.put(None)
+                nb = sum(len(g) for g in self.groups)
+                print(f'# epoch {self.epoch}: {nb} batches in {len(self.groups)} launches of <= {self.G}, '
+                      f'host enqueue {self._t_pipeline * 1e3 / max(1, nb):.3f} ms/batch', flush=True)
+            self._put(None)
         except BaseException as e:  # surface worker errors to the consumer
             self.error = e
-            self.output_queue.put(None)
+            self._put(None, force=True)
 
-    def run_pipeline(self, b_ix, batch_indices, batch_slot, cuda_event):
-        self.memory_context.start_batch(b_ix)
-        ctx = self.contexts[batch_slot]
-        self._check_status(batch_slot, wait=True)
+    def _acquire(self, s):
+        """Wait until the consumer released set s (host side)."""
+        with self._cv:
+            while not self._released[s]:
+                if self.terminate_event.is_set():
+                    return False
+                self._cv.wait(0.1)
+            self._released[s] = False
+            return not self.terminate_event.is_set()
+
+    def _put(self, item, force=False):
+        while True:
+            try:
+                self.output_queue.put(item, block=True, timeout=0.5)
+                return True
+            except Full:
+                if self.terminate_event.is_set():
+                    if force:
+                        try:
+                            self.output_queue.get_nowait()
+                        except Empty:
+                            pass
+                        continue
+                    return False
+
+    def _put_group(self, s, group, results):
+        bs = self.loader.batch_size
+        n = len(group)
+        for j, batch in enumerate(group):
+            lo, hi = j * bs, j * bs + len(batch)
+            res = tuple(r[lo:hi] for r in results) if n > 1 else results
+            if not self._put((s, res, j == n - 1)):
+                return False
+        return True
+
+    def run_pipeline(self, m, group, s):
+        self.memory_context.start_batch(m)
+        ctx = self.contexts[s]
+        self._check_status(s)
+        indices = np.concatenate(group) if len(group) > 1 else group[0]
         if self.is_cuda:
-            stream = self.cuda_streams[batch_slot]
+            stream = self.cuda_streams[s]
             with ch.cuda.stream(stream):
-                if cuda_event:
-                    cuda_event.wait()
+                ev = self._release_event[s]
+                if ev is not None:
+                    stream.wait_event(ev)
                 runtime.set_current(ctx)
-                ctx.begin_batch(batch_indices, self.epoch, stream)
-                result = self.loader.graph.run(batch_indices, ctx, self.memory_allocations, batch_slot)
-                ctx.end_batch(self._queue_status(batch_slot, ctx, stream))
+                ctx.begin_batch(indices, self.epoch, stream)
+                result = self.loader.graph.run(indices, ctx, self.memory_allocations, s)
+                ctx.end_batch(self._queue_status(s, ctx, stream))
         else:
             runtime.set_current(ctx)
-            ctx.begin_batch(batch_indices, self.epoch, None)
-            result = self.loader.graph.run(batch_indices, ctx, self.memory_allocations, batch_slot)
+            ctx.begin_batch(indices, self.epoch, None)
+            result = self.loader.graph.run(indices, ctx, self.memory_allocations, s)
         runtime.set_current(None)
         return result
 
     # ------------------------------------------------- decode status check --
-    def _queue_status(self, slot, ctx, stream):
-        """Copy this batch's per-sample status words to pinned host memory
+    def _queue_status(self, s, ctx, stream):
+        """Copy this launch's per-sample status words to pinned host memory
         and record an event after them; returns that event (None if no
         status is pending)."""
         if not ctx.pending_status:
-            self._status[slot] = None
+            self._status[s] = None
             return None
         from .. import libffcv as L
         recs = []
@@ -193,43 +256,60 @@ class EpochIterator(Thread):
             recs.append((host, what))
         ev = ch.cuda.Event()
         ev.record(stream)
-        self._status[slot] = (ev, recs, np.asarray(ctx.batch_indices).copy())
+        self._status[s] = (ev, recs, np.asarray(ctx.batch_indices).copy())
         return ev
 
-    def _check_status(self, slot, wait=False):
-        rec = self._status[slot]
+    def _check_status(self, s):
+        rec = self._status[s]
         if rec is None:
             return
         ev, recs, ids = rec
-        if not wait and not ev.query():
-            return
         ev.synchronize()
-        self._status[slot] = None
+        self._status[s] = None
         from ..libffcv import SAMPLE_STATUS
         for host, what in recs:
-            st = host.numpy()
+            st = host.numpy().reshape(-1)
             bad = np.nonzero(st)[0]
             if bad.size:
                 k = int(bad[0])
+                code = int(st[k])
                 msg = (f'{what}: sample {int(ids[k])} failed to decode: '
-                       f'{SAMPLE_STATUS.get(int(st[k]), st[k])} ({bad.size} bad in batch)')
+                       f'{SAMPLE_STATUS.get(code, code)} ({bad.size} bad in launch)')
                 self.error = DecodeError(msg)
 
     # ----------------------------------------------------------- consumer --
+    def _release_pending(self):
+        """The consumer is done enqueueing work on the set it held last."""
+        s = self._pending_release
+        if s is None:
+            return
+        self._pending_release = None
+        ev = None
+        if self.is_cuda:
+            ev = ch.cuda.Event()
+            ev.record(self.current_stream)
+        with self._cv:
+            self._release_event[s] = ev
+            self._released[s] = True
+            self._cv.notify_all()
+
     def __next__(self):
-        result = self.output_queue.get()
-        if result is None:
-            if self.is_cuda:
-                for s in range(len(self._status)):
-                    self._check_status(s, wait=True)
+        self._release_pending()
+        item = self.output_queue.get()
+        if item is None:
+            self.join()
+            if self.is_cuda and self.error is None:
+                for s in range(self.n_sets):
+                    self._check_status(s)
             self.close()
             if self.error is not None:
                 raise self.error
             raise StopIteration()
-        slot, result = result
+        s, result, last = item
         if self.is_cuda:
-            stream = self.cuda_streams[slot]
-            self.current_stream.wait_stream(stream)
+            self.current_stream.wait_stream(self.cuda_streams[s])
+        if last:
+            self._pending_release = s
         if self.error is not None:
             self.close()
             raise self.error
@@ -239,10 +319,19 @@ class EpochIterator(Thread):
         return self
 
     def close(self):
+        """Stop the producer (also for an iterator abandoned mid-epoch) and
+        release the memory manager's epoch context."""
         self.terminate_event.set()
+        with self._cv:
+            self._cv.notify_all()
+        if self.is_alive() and threading.current_thread() is not self:
+            self.join()
         if not self.closed:
             self.closed = True
             self.memory_context.__exit__(None, None, None)
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -108,6 +108,10 @@ class Loader:
     device_cache : bool (keyword only, new)
         Keep the whole .beton resident in HBM (default) or stage each
         batch's bytes through pinned memory.
+    batches_per_launch : int, optional (keyword only, new)
+        Consecutive batches decoded by one launch sequence when every
+        operation is per-sample (default: enough batches for ~6k samples,
+        which fills the MI355X; 1 when the graph mixes samples).
     """
 
     def __init__(self, fname: str, batch_size: int, num_workers: int = -1,
@@ -117,7 +121,7 @@ class Loader:
                  pipelines: Mapping[str, Sequence[Union[Operation, ch.nn.Module]]] = {},
                  custom_fields: Mapping[str, Type[Field]] = {}, drop_last: bool = True,
                  batches_ahead: int = 3, recompile: bool = False, order_kwargs: dict = dict(),
-                 *, device=None, device_cache: bool = True):
+                 *, device=None, device_cache: bool = True, batches_per_launch: int = None):
         if distributed and order == OrderOption.RANDOM and (seed is None):
             print('Warning: no ordering seed was specified with distributed=True. '
                   'Setting seed to 0 to match PyTorch distributed sampler.')
@@ -131,7 +135,10 @@ class Loader:
             'indices': indices, 'pipelines': pipelines, 'drop_last': drop_last,
             'batches_ahead': batches_ahead, 'recompile': recompile, 'device': device,
             'device_cache': device_cache, 'custom_fields': custom_fields,
+            'batches_per_launch': batches_per_launch,
         }
+        self.batches_per_launch = batches_per_launch
+        self._active_iterator = None
         self.fname: str = fname
         self.batch_size: int = batch_size
         self.batches_ahead = batches_ahead
@@ -223,7 +230,14 @@ class Loader:
         self.next_epoch += 1
         if self.code is None or self.recompile:
             self.generate_code()
-        return EpochIterator(self, selected_order)
+        # an iterator abandoned mid-epoch (break out of the loop) must stop
+        # before the next epoch re-uses the shared buffer sets
+        prev, self._active_iterator = self._active_iterator, None
+        if prev is not None:
+            prev.close()
+        it = EpochIterator(self, selected_order)
+        self._active_iterator = it
+        return it
 
     def filter(self, field_name: str, condition: Callable[[Any], bool]) -> 'Loader':
         new_args = {**self._args}

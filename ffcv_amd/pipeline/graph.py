@@ -37,6 +37,7 @@ INITIAL_STATE = State(jit_mode=True, device=ch.device('cpu'), dtype=np.dtype('u1
 class _ToHost(Operation):
     """Implicit device -> pinned host transfer (graph-inserted)."""
     device_aware = True
+    per_sample = True
 
     def __init__(self, as_tensor=False):
         super().__init__()
@@ -256,10 +257,38 @@ class Graph:
             self.collect_requirements()
         return self.exec_nodes, [self.outputs[k].id for k in self.leaf_nodes]
 
+    def groupable(self):
+        """True when every operation treats samples independently, so that
+        consecutive batches may run through the graph as one launch."""
+        if not self._finalized:
+            self.collect_requirements()
+        return all(getattr(n.operation, 'per_sample', False) for n in self.exec_nodes)
+
+    def allocation_signature(self):
+        """The allocations in execution order, independent of node ids."""
+        if not self._finalized:
+            self.collect_requirements()
+
+        def desc(q):
+            if isinstance(q, AllocationQuery):
+                return (tuple(int(x) for x in q.shape), str(q.dtype), str(q.device))
+            if isinstance(q, Sequence):
+                return tuple(desc(x) for x in q)
+            return None
+        return tuple((type(n.operation).__name__, desc(self.allocations[n.id])) for n in self.exec_nodes)
+
+    def rebind_memory(self, memory):
+        """Buffers allocated for an earlier collect_requirements() with the
+        same allocation_signature(), re-keyed to the current node ids."""
+        order = memory['__order__']
+        new = {n.id: memory[old] for n, old in zip(self.exec_nodes, order)}
+        new['__order__'] = [n.id for n in self.exec_nodes]
+        return new
+
     def allocate_memory(self, batch_size, batches_ahead):
         if not self._finalized:
             self.collect_requirements()
-        memory = {}
+        memory = {'__order__': [n.id for n in self.exec_nodes]}
         for node_id, q in self.allocations.items():
             if isinstance(q, AllocationQuery):
                 memory[node_id] = allocate_query(q, batch_size, batches_ahead)

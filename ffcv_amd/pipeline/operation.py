@@ -11,6 +11,12 @@ semantics; there is no numba here).
 Operations that know how to run on a HIP device set the class attribute
 ``device_aware = True``; the graph inserts a device->host transfer in
 front of any other operation that receives device-resident data.
+
+``per_sample = True`` declares that the operation treats every sample of a
+batch independently (no batch-level mixing such as ImageMixup): the
+EpochIterator may then run several consecutive batches through the graph as
+one launch (one decode launch fills the GPU) and hand them out one by one.
+Unknown user operations default to False, which keeps one batch per run.
 """
 from abc import ABC, abstractmethod
 from typing import TYPE_CHECKING, Callable, Optional, Tuple
@@ -26,6 +32,7 @@ if TYPE_CHECKING:
 
 class Operation(ABC):
     device_aware = False
+    per_sample = False
 
     def __init__(self):
         self.metadata: np.ndarray = None

@@ -10,6 +10,7 @@ from ..pipeline.state import State
 class Squeeze(Operation):
     """Remove given dimensions of input of size 1."""
     device_aware = True
+    per_sample = True
 
     def __init__(self, *dims):
         super().__init__()

@@ -30,6 +30,7 @@ class Cutout(Operation):
         An RGB color ((0, 0, 0) by default) to fill the cutout square with.
     """
     device_aware = True
+    per_sample = True
 
     def __init__(self, crop_size: int, fill: Tuple[int, int, int] = (0, 0, 0)):
         super().__init__()

@@ -27,6 +27,7 @@ class RandomHorizontalFlip(Operation):
         The probability with which to flip each image in the batch horizontally.
     """
     device_aware = True
+    per_sample = True
 
     def __init__(self, flip_prob: float = 0.5):
         super().__init__()

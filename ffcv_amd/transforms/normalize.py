@@ -38,6 +38,7 @@ class NormalizeImage(Operation):
         The desired output type (numpy dtype).
     """
     device_aware = True
+    per_sample = True
 
     def __init__(self, mean: np.ndarray, std: np.ndarray, type: np.dtype):
         super().__init__()
@@ -68,9 +69,9 @@ class NormalizeImage(Operation):
         return self.generate_code_gpu()
 
     def generate_code_gpu(self) -> Callable:
+        # any table dtype, like the reference's templated cupy kernel
+        # (normalize.py:64-65): the kernel gathers element bit patterns
         final_type = ch_dtype_from_numpy(self.original_dtype)
-        if final_type != ch.float16:
-            raise NotImplementedError('device NormalizeImage supports float16 output')
 
         def normalize_convert(images, result):
             from .. import libffcv as L
@@ -79,8 +80,7 @@ class NormalizeImage(Operation):
             assert images.is_contiguous(memory_format=ch.channels_last), 'Images need to be in channel last'
             result = result[:B]
             flat = images.permute(0, 2, 3, 1)
-            L.normalize_batch(flat, self.device_lut(images.device), result,
-                              ctx.stream if ctx else None)
+            L.lut_batch(flat, self.device_lut(images.device), result, ctx.stream if ctx else None)
             final_result = result.reshape(B, H, W, C).permute(0, 3, 1, 2)
             return final_result.view(final_type)
         return normalize_convert

@@ -26,6 +26,7 @@ def _torch_dtype(dtype):
 class ToTensor(Operation):
     """Convert from Numpy array to PyTorch Tensor."""
     device_aware = True
+    per_sample = True
 
     def __init__(self):
         super().__init__()
@@ -53,6 +54,7 @@ class ToDevice(Operation):
         Asynchronous if copying from CPU to GPU.
     """
     device_aware = True
+    per_sample = True
 
     def __init__(self, device, non_blocking=True):
         super().__init__()
@@ -96,6 +98,7 @@ class ToTorchImage(Operation):
         Convert to float16.
     """
     device_aware = True
+    per_sample = True
 
     def __init__(self, channels_last=True, convert_back_int16=True):
         super().__init__()
@@ -133,6 +136,7 @@ class ToTorchImage(Operation):
 class Convert(Operation):
     """Convert to target data type (ops.py:114-136)."""
     device_aware = True
+    per_sample = True
 
     def __init__(self, target_dtype):
         super().__init__()
@@ -151,6 +155,7 @@ class Convert(Operation):
 class View(Operation):
     """View array using np.view or torch.view (ops.py:139-160)."""
     device_aware = True
+    per_sample = True
 
     def __init__(self, target_dtype):
         super().__init__()

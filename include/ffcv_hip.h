@@ -216,8 +216,13 @@ int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *ctx, void *stream,
 int ffcv_cutout_batch(void *stream, uint8_t *images, int batch, int height,
                       int width, const int32_t *cutout_yx, int crop_size,
                       const uint8_t fill[3]);
-/* normalize.py:65 cupy kernel: out[i] = lut[in[i]*3 + i%3] over n elements
- * of a channels-last uint8 batch; out holds fp16 bits. */
+/* normalize.py:64-65 cupy ElementwiseKernel 'output = table[input*3 + i%3]'
+ * (templated on the output type T there): out[i] = lut[in[i]*3 + i%3] over n
+ * elements of a channels-last uint8 batch.  lut: device [256][3] table of
+ * elem_bytes-wide elements (1, 2, 4 or 8: u8/int16/fp16/fp32/f64 ...). */
+int ffcv_lut_batch(void *stream, const uint8_t *in, uint64_t n,
+                   const void *lut, int elem_bytes, void *out);
+/* ffcv_lut_batch with a fp16 (int16 bits) table (normalize.py:45-48). */
 int ffcv_normalize_batch(void *stream, const uint8_t *in, uint64_t n,
                          const uint16_t *lut, uint16_t *out);
 /* flip.py:35-40: dst[i] = images[i, :, ::-1] where flips[i] != 0. */

@@ -258,3 +258,133 @@ def test_process_cache_pcie_matches_device_cache(tmpdir_m, mode, n):
             assert ch.equal(ia.view(ch.int16), ib.view(ch.int16))
             seen += len(lb)
         assert seen == n
+
+
+@pytest.mark.parametrize('dtype', [np.float16, np.float32])
+def test_gpu_normalization_standalone(tmpdir_m, dtype):
+    """test_image_normalization.py:71-108 (test_gpu_normalization) ported:
+    SimpleRGB -> ToTensor -> ToDevice -> ToTorchImage -> NormalizeImage ->
+    View runs the standalone device LUT kernel (ffcv_lut_batch).  Checked
+    exactly against the reference's LUT arithmetic (normalize.py:42-49) and
+    with the reference's own np.allclose assertion; fp16 and fp32 tables."""
+    from ffcv_amd.transforms import View
+    fn = os.path.join(tmpdir_m, 'norm_raw.beton')
+    if not os.path.exists(fn):
+        write(fn, ConstDS(500, hw=(25, 30)), {'index': IntField(), 'value': RGBImageField(write_mode='raw')})
+    mean, std = np.array([0, 1, 2]), np.array([1, 10, 20])
+    tdt = ch.float16 if dtype == np.float16 else ch.float32
+    loader = Loader(fn, batch_size=5, num_workers=2, pipelines={'value': [
+        SimpleRGBImageDecoder(), ToTensor(), ToDevice(ch.device('cuda:0')), ToTorchImage(),
+        NormalizeImage(mean, std, dtype), View(tdt)]})
+    table = ((np.arange(256)[:, None] - mean[None, :]) / std[None, :]).astype(dtype)
+    seen = 0
+    for index, images in loader:
+        assert images.dtype == tdt and images.shape[1:] == (3, 25, 30)
+        got = images.cpu().numpy()
+        for k, i in enumerate(index.reshape(-1).tolist()):
+            v = i % 255
+            want = np.broadcast_to(table[v][:, None, None], (3, 25, 30))
+            assert np.array_equal(np.ascontiguousarray(got[k]).view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
+            ref = np.full((3, 25, 30), v, dtype)
+            ref -= mean[:, None, None]
+            ref /= std[:, None, None]
+            assert np.allclose(ref, got[k])
+            seen += 1
+    assert seen == 500
+
+
+def test_flip_unfused_device(tmpdir_m):
+    """RandomHorizontalFlip after a Simple decoder runs the standalone device
+    flip kernel (ffcv_flip_batch) with the contract's per-sample decisions."""
+    from ffcv_amd.transforms.rng import contract_seed
+    fn = os.path.join(tmpdir_m, 'flip_raw.beton')
+    ds = NaturalDS(30, hw=(20, 26), seed=5)
+    write(fn, ds, {'image': RGBImageField(write_mode='raw'), 'label': IntField()})
+    loader = Loader(fn, batch_size=8, seed=4, drop_last=False, pipelines={
+        'image': [SimpleRGBImageDecoder(), RandomHorizontalFlip(0.5), ToTensor(), ToDevice('cuda:0')]})
+    flipped = 0
+    for b, (images, labels) in enumerate(loader):
+        got = images.cpu().numpy()
+        for k in range(got.shape[0]):
+            sid = b * 8 + k
+            u = np.random.RandomState(contract_seed(4, 0, sid, 3)).uniform(0, 1)
+            want = ds.imgs[sid][:, ::-1] if u < 0.5 else ds.imgs[sid]
+            flipped += u < 0.5
+            assert np.array_equal(got[k], want), sid
+    assert 0 < flipped < 30
+
+
+def _c3_loader(fn, seed, out=(64, 64), **kw):
+    return Loader(fn, batch_size=16, order=OrderOption.RANDOM, seed=seed, pipelines={
+        'image': [RandomResizedCropRGBImageDecoder(out), Cutout(12, (124, 116, 103)), ToTensor(),
+                  ToDevice(ch.device('cuda:0'), non_blocking=True), ToTorchImage(),
+                  NormalizeImage(MEAN, STD, np.float16)],
+        'label': [IntDecoder(), ToTensor(), ToDevice('cuda:0')]}, **kw)
+
+
+def test_launch_groups_match_single_batches(tmpdir_m):
+    """Several batches per decode launch (the default) hand out exactly the
+    batches one launch per batch gives, including a partial last batch."""
+    fn = os.path.join(tmpdir_m, 'grp.beton')
+    write(fn, NaturalDS(100, hw=(80, 96), var=True, seed=6),
+          {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    a = _c3_loader(fn, 7, drop_last=False, batches_per_launch=1)
+    b = _c3_loader(fn, 7, drop_last=False)
+    c = _c3_loader(fn, 7, drop_last=False, batches_per_launch=3)
+    for epoch in range(2):
+        n = 0
+        for (ia, la), (ib, lb), (ic, lc) in zip(a, b, c):
+            assert ch.equal(la, lb) and ch.equal(la, lc)
+            assert ch.equal(ia.view(ch.int16), ib.view(ch.int16))
+            assert ch.equal(ia.view(ch.int16), ic.view(ch.int16))
+            n += len(la)
+        assert n == 100
+
+
+@pytest.mark.parametrize('recompile', [False, True])
+def test_output_size_change_between_epochs(tmpdir_m, oracle, recompile):
+    """Progressive resizing: a new decoder output_size between epochs takes
+    effect (new buffers, new kernel target), with or without recompile
+    (making_dataloaders.rst: a resolution change needs no recompile)."""
+    fn = os.path.join(tmpdir_m, 'resz.beton')
+    if not os.path.exists(fn):
+        write(fn, NaturalDS(48, hw=(90, 110), var=True, seed=9),
+              {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    samples = _samples(fn)
+    lut = oracle.normalize_lut(MEAN, STD)
+    loader = _c3_loader(fn, 3, recompile=recompile)
+    dec = loader.pipeline_specs['image'].decoder
+    for epoch, size in enumerate([(64, 64), (48, 40), (72, 80)]):
+        dec.output_size = size
+        order = np.random.default_rng(3 + epoch).permutation(48)
+        for b, (images, labels) in enumerate(loader):
+            assert images.shape == (16, 3) + size
+            ids = order[b * 16:(b + 1) * 16]
+            want = _expected(oracle, samples, ids, 3, epoch, size, cutout=12, fill=(124, 116, 103), lut=lut)
+            got = images.permute(0, 2, 3, 1).cpu().numpy()
+            assert np.array_equal(got.view(np.uint16), want.view(np.uint16))
+
+
+def test_early_break_then_next_epoch(tmpdir_m, oracle):
+    """An iterator abandoned after one batch is stopped before the next
+    epoch re-uses the buffer sets; the next epoch is exact."""
+    fn = os.path.join(tmpdir_m, 'brk.beton')
+    write(fn, NaturalDS(160, hw=(64, 80), var=True, seed=2),
+          {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    samples = _samples(fn)
+    lut = oracle.normalize_lut(MEAN, STD)
+    loader = _c3_loader(fn, 11, batches_per_launch=2)
+    for _ in loader:
+        break
+    for epoch in (1, 2):
+        order = np.random.default_rng(11 + epoch).permutation(160)
+        n = 0
+        for b, (images, labels) in enumerate(loader):
+            ids = order[b * 16:(b + 1) * 16]
+            want = _expected(oracle, samples, ids, 11, epoch, (64, 64), cutout=12, fill=(124, 116, 103), lut=lut)
+            assert np.array_equal(images.permute(0, 2, 3, 1).cpu().numpy().view(np.uint16), want.view(np.uint16))
+            assert (labels.cpu().numpy().reshape(-1) == ids % 10).all()
+            n += 1
+            if epoch == 1 and b == 4:
+                break  # abandon again mid-epoch
+        assert n == (5 if epoch == 1 else 10)

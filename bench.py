@@ -202,6 +202,8 @@ def main():
                     help='decode launches in flight on separate HIP streams (default per config)')
     ap.add_argument('--unfused', action='store_true',
                     help='separate gather / draw kernels before the decode (the Loader\'s staged path)')
+    ap.add_argument('--no-host-check', action='store_true',
+                    help='profiling runs: do not fail when submission dominates (the profiler slows the host)')
     ap.add_argument('--lib', default=None, help='diagnostic A/B: load this build of libffcv_hip.so')
     ap.add_argument('--k2flags', type=int, default=0, help='diagnostic: K2 timing-only flags')
     ap.add_argument('--only', type=int, default=0,
@@ -420,48 +422,50 @@ def main():
         crops_np = slots[(launch_no[0] - 1) % S]['crops'][:launch_imgs[-1]].cpu().numpy()
         unit_bytes = float((crops_np[:, 2].astype(np.float64) * crops_np[:, 3] * 3).mean()) + out * out * 3
         roof_note = '3*h*w crop ROI read + 448*448*3 write per image (SURVEY 8d C5)'
-    # per-launch figures from HIP events on the slot stream (full launches only)
-    mean_launch_ms = float(np.mean(launch_ms))
+    # Roofline.  Launches overlap by design (S in flight), so one launch's
+    # HIP-event duration includes GPU time it shares with the others; the
+    # per-launch figure uses each launch's share of the timed region
+    # (elapsed / launches), i.e. work per image x images/s.  The raw event
+    # durations are reported beside it.
+    n_launch = len(launch_ms)
     imgs_per_launch = float(np.mean(launch_imgs))
-    hbm_achieved = unit_bytes * imgs_per_launch / (mean_launch_ms * 1e-3) / 1e9
+    eff_launch_ms = elapsed * 1e3 / n_launch
+    per_gpu_rate = value / world
+    hbm_achieved = unit_bytes * per_gpu_rate / 1e9
     hbm = {'bound': 'hbm', 'achieved': round(hbm_achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(hbm_achieved / HBM_PEAK_GBS, 5), 'traffic': None,
-           'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note,
-           'job_achieved': round(value / world * unit_bytes / 1e9, 2),
-           'job_frac': round(value / world * unit_bytes / 1e9 / HBM_PEAK_GBS, 5)}
+           'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note}
     kernels = (['jpeg_entropy_kernel<0>', 'jpeg_color_resize_kernel<0, true>' if norm else
                 'jpeg_color_resize_kernel<0, false>'] if mode == 'jpg' else ['rrc_raw_kernel<false>'])
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
-    # (tools/profile.sh -> tools/pmc_summary.py), per image x images per launch
+    # (tools/profile.sh -> tools/pmc_summary.py): bytes per image x images per launch
     pm = load_profile(f'traffic_{args.config}.json')
-    if pm and all(n in pm and 'fetch_size_kb' in pm[n] and 'write_size_kb' in pm[n] for n in kernels):
-        per_img = sum((pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 / pm[n].get('images', 1)
-                      for n in kernels) if all('images' in pm[n] for n in kernels) else None
-        if per_img is not None:
-            hbm['traffic'] = round(per_img * imgs_per_launch, 1)
-            hbm['traffic_note'] = (f'HBM bytes per launch of {imgs_per_launch} images (FETCH_SIZE + '
-                                   f'WRITE_SIZE per image, rocprofv3 PMC, profiles/traffic_{args.config}.json); '
-                                   f'algorithmic {unit_bytes * imgs_per_launch:.0f}')
-    roof = dict(hbm)
-    roof['kernel'] = ' + '.join(kernels) + f' (one launch of {imgs_per_launch} images, HIP events on the slot stream)'
-    roof['launch_ms'] = round(mean_launch_ms, 4)
+    if pm and all(n in pm and 'fetch_size_kb' in pm[n] and 'write_size_kb' in pm[n] and 'images' in pm[n]
+                  for n in kernels):
+        per_img = sum((pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 / pm[n]['images'] for n in kernels)
+        hbm['traffic'] = round(per_img * imgs_per_launch, 1)
+        hbm['traffic_per_image'] = round(per_img, 1)
+        hbm['traffic_note'] = (f'HBM bytes per launch of {imgs_per_launch:.0f} images (FETCH_SIZE + WRITE_SIZE, '
+                               f'rocprofv3 PMC, profiles/traffic_{args.config}.json, build {pm.get("_build")}); '
+                               f'algorithmic {unit_bytes * imgs_per_launch:.0f}')
+    launch = {'kernel': ' + '.join(kernels) + f' (launches of {imgs_per_launch:.0f} images)',
+              'launches': n_launch, 'launch_ms': round(eff_launch_ms, 4),
+              'launch_ms_events': round(float(np.mean(launch_ms)), 4)}
+    roof = dict(hbm, **launch)
     sq = load_profile(f'sq_{args.config}.json')
     if mode == 'jpg' and sq and all(n in sq for n in kernels):
         # the JPEG path is bound by instruction issue / latency of the serial
         # Huffman chain, not HBM: VALU wave-instructions per
-        # image (SQ_INSTS_VALU, current build) x images per launch / launch time
+        # image (SQ_INSTS_VALU, rocprofv3) x images/s
         valu_img = sum(sq[n]['valu_per_image'] for n in kernels)
-        issue = valu_img * imgs_per_launch / (mean_launch_ms * 1e-3) / 1e9
-        job_issue = valu_img * value / world / 1e9
+        issue = valu_img * per_gpu_rate / 1e9
         roof = {'bound': 'issue', 'achieved': round(issue, 2), 'peak': VALU_PEAK_GIPS,
                 'unit': 'G VALU wave-instr/s', 'frac': round(issue / VALU_PEAK_GIPS, 4),
-                'traffic': hbm['traffic'],
-                'kernel': roof['kernel'], 'launch_ms': roof['launch_ms'],
-                'valu_per_image': round(valu_img, 1),
-                'job_achieved': round(job_issue, 2), 'job_frac': round(job_issue / VALU_PEAK_GIPS, 4),
-                'note': (f'SQ_INSTS_VALU per image from profiles/sq_{args.config}.json (rocprofv3 --pmc, '
-                         f'{sq.get("_build", "current build")}); peak = 1024 SIMDs x 2.4 GHz / 2 cycles '
-                         f'per wave64 VALU op'),
+                'traffic': hbm['traffic'], **launch,
+                'valu_per_image': {n: round(sq[n]['valu_per_image'], 1) for n in kernels},
+                'note': (f'SQ_INSTS_VALU per image from profiles/sq_{args.config}.json (rocprofv3 --pmc, build '
+                         f'{sq.get("_build")}) x images/s; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 '
+                         f'VALU instruction'),
                 'hbm': hbm}
     res = {
         'metric': 'device-resident images/s, JPEG->RRC 224x224 batch 512; HBM GB/s vs peak',
@@ -495,7 +499,7 @@ def main():
     # a host-bound measurement is not a measurement of the path (VERDICT r1:
     # 1.87 of 2.07 ms per step was submission).  Submission is asynchronous, so
     # it only bounds the region as it approaches the wall time; 25% margin.
-    if host_ms_per_step > 0.25 * ms_per_step:
+    if host_ms_per_step > 0.25 * ms_per_step and not args.no_host_check:
         print(f'bench: ERROR host submission {host_ms_per_step:.3f} ms/step is more than 25% of '
               f'{ms_per_step:.3f} ms/step: the timed region is host-bound', file=sys.stderr, flush=True)
         sys.exit(3)

@@ -21,7 +21,12 @@ in four modes and prints one JSON line per mode:
   * pcie_in_process_cache : as pcie_in with os_cache=False: the page scheduler
                      preads the batches' .beton pages into a slot pool and
                      the native gather reads the samples out of the slots
-Images/s is measured over whole epochs after one warm-up epoch.
+  * link           : bare pinned hipMemcpyAsync H2D and D2H rates of one
+                     decoded fp16 batch (154 MB), the ceiling of pcie_in_out
+Images/s is measured over whole epochs after one warm-up epoch.  In
+pcie_in_out the decoded batches leave on a dedicated copy stream into a
+ring of pinned host buffers (double-buffered), so the D2H of batch b
+overlaps the decode of the following batches.
 """
 import argparse
 import json
@@ -43,7 +48,7 @@ def main():
     ap.add_argument('--epochs', type=int, default=2)
     ap.add_argument('--batch', type=int, default=512)
     ap.add_argument('--dir', default=None)
-    ap.add_argument('--modes', default='device_cache,pcie_in,pcie_in_out,pcie_in_process_cache')
+    ap.add_argument('--modes', default='link,device_cache,pcie_in,pcie_in_out,pcie_in_process_cache')
     args = ap.parse_args()
 
     import torch
@@ -75,6 +80,9 @@ def main():
               file=sys.stderr)
     dev = torch.device('cuda:0')
     for mode in args.modes.split(','):
+        if mode == 'link':
+            print(json.dumps(link_rates(torch, dev, args.batch * 224 * 224 * 3 * 2)), flush=True)
+            continue
         loader = Loader(fn, batch_size=args.batch, order=OrderOption.RANDOM, seed=0, drop_last=True,
                         device=dev, device_cache=(mode == 'device_cache'),
                         os_cache=(mode != 'pcie_in_process_cache'),
@@ -85,7 +93,11 @@ def main():
                                    'label': [IntDecoder(), ToTensor(), ToDevice(dev)]})
         # the batch comes back in its channels-last memory order (the
         # ToTorchImage view's storage), so the D2H copy is one memcpy
-        host = torch.empty((args.batch, 224, 224, 3), dtype=torch.float16).pin_memory()
+        nbuf = 3
+        hosts = [torch.empty((args.batch, 224, 224, 3), dtype=torch.float16).pin_memory() for _ in range(nbuf)]
+        copy_stream = torch.cuda.Stream(dev)
+        copied = [None] * nbuf
+        k = 0
         n_img = 0
         t0 = None
         for ep in range(args.epochs + 1):
@@ -94,7 +106,17 @@ def main():
                 t0 = time.perf_counter()
             for images, labels in loader:
                 if mode == 'pcie_in_out':
-                    host.copy_(images.permute(0, 2, 3, 1), non_blocking=True)
+                    slot = k % nbuf
+                    if copied[slot] is not None:
+                        copied[slot].synchronize()  # the host buffer is free again
+                    copy_stream.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(copy_stream):
+                        hosts[slot].copy_(images.permute(0, 2, 3, 1), non_blocking=True)
+                        images.record_stream(copy_stream)
+                        ev = torch.cuda.Event()
+                        ev.record(copy_stream)
+                    copied[slot] = ev
+                    k += 1
                 if ep >= 1:
                     n_img += images.shape[0]
         torch.cuda.synchronize()
@@ -102,6 +124,23 @@ def main():
         print(json.dumps({'mode': mode, 'images_per_s': round(n_img / el, 1), 'images': n_img,
                           'seconds': round(el, 3), 'batch': args.batch, 'dataset': args.n,
                           'beton_mb': round(os.path.getsize(fn) / 1e6, 1)}), flush=True)
+
+
+def link_rates(torch, dev, nbytes, reps=20):
+    """Pinned host <-> HBM copy rates (GB/s) for a buffer of nbytes."""
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    out = {'mode': 'link', 'bytes': nbytes}
+    for name, dst, src in (('h2d', d, h), ('d2h', h, d)):
+        for _ in range(3):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        out[name + '_gbs'] = round(nbytes * reps / (time.perf_counter() - t0) / 1e9, 2)
+    return out
 
 
 def _encode_prepared(self, destination, item, malloc):

@@ -10,6 +10,44 @@
 #include "../../include/ffcv_hip.h"
 
 #define FFCV_DEV __device__ __forceinline__
+// The INTER_AREA restatement below is single-source: the kernels run it per
+// output pixel and the host C-ABI resize() (csrc/ffcv_host.hip, the
+// reference's libffcv.cpp:33-42 signature) runs the very same functions on
+// the CPU.  These helpers pick the gfx950 instruction on the device pass.
+#define FFCV_HD __host__ __device__ __forceinline__
+
+FFCV_HD int ffcv_f2i_rn(float x) {  // round half to even, like cvRound
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __float2int_rn(x);
+#else
+  return (int)nearbyintf(x);
+#endif
+}
+FFCV_HD int ffcv_mul24(int a, int b) {  // operands < 2^23 in magnitude here
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __mul24(a, b);
+#else
+  return a * b;
+#endif
+}
+FFCV_HD uint32_t ffcv_f2u_bits(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __float_as_uint(x);
+#else
+  uint32_t u;
+  __builtin_memcpy(&u, &x, 4);
+  return u;
+#endif
+}
+FFCV_HD float ffcv_u2f_bits(uint32_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __uint_as_float(u);
+#else
+  float x;
+  __builtin_memcpy(&x, &u, 4);
+  return x;
+#endif
+}
 
 // --------------------------------------------------------------------------
 // MT19937 with O(1) state.
@@ -35,19 +73,19 @@ struct DevMT {
   int err;
 };
 
-FFCV_DEV uint32_t mt_chain(uint32_t x, uint32_t k) { return 1812433253u * (x ^ (x >> 30)) + k; }
-FFCV_DEV uint32_t mt_temper(uint32_t y) {
+FFCV_HD uint32_t mt_chain(uint32_t x, uint32_t k) { return 1812433253u * (x ^ (x >> 30)) + k; }
+FFCV_HD uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
   y ^= (y << 15) & 0xefc60000u;
   y ^= (y >> 18);
   return y;
 }
-FFCV_DEV uint32_t mt_twist1(uint32_t lo_src, uint32_t hi_next, uint32_t far) {
+FFCV_HD uint32_t mt_twist1(uint32_t lo_src, uint32_t hi_next, uint32_t far) {
   uint32_t y = (lo_src & 0x80000000u) | (hi_next & 0x7fffffffu);
   return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
-FFCV_DEV void mt_init(DevMT &m, uint32_t seed) {
+FFCV_HD void mt_init(DevMT &m, uint32_t seed) {
   m.seed = seed;
   m.a0 = seed;
   m.a1 = mt_chain(seed, 1);
@@ -57,17 +95,17 @@ FFCV_DEV void mt_init(DevMT &m, uint32_t seed) {
   m.n = 0;
   m.err = 0;
 }
-__device__ __noinline__ uint32_t mt_old_at(uint32_t seed, int k) {
+static __host__ __device__ __noinline__ uint32_t mt_old_at(uint32_t seed, int k) {
   uint32_t x = seed;
   for (int i = 1; i <= k; i++) x = mt_chain(x, (uint32_t)i);
   return x;
 }
-__device__ __noinline__ uint32_t mt_new_at(uint32_t seed, int m) {
+static __host__ __device__ __noinline__ uint32_t mt_new_at(uint32_t seed, int m) {
   if (m < 227) return mt_twist1(mt_old_at(seed, m), mt_old_at(seed, m + 1), mt_old_at(seed, m + 397));
   if (m < 623) return mt_twist1(mt_old_at(seed, m), mt_old_at(seed, m + 1), mt_new_at(seed, m - 227));
   return mt_twist1(mt_old_at(seed, 623), mt_new_at(seed, 0), mt_new_at(seed, 396));
 }
-FFCV_DEV uint32_t mt_u32(DevMT &m) {
+FFCV_HD uint32_t mt_u32(DevMT &m) {
   uint32_t v;
   if (m.n < 227) {
     v = mt_twist1(m.a0, m.a1, m.b);
@@ -84,17 +122,17 @@ FFCV_DEV uint32_t mt_u32(DevMT &m) {
   return mt_temper(v);
 }
 // genrand_res53 == numpy mt19937_next_double == numba get_next_double
-FFCV_DEV double mt_double(DevMT &m) {
+FFCV_HD double mt_double(DevMT &m) {
   int32_t a = (int32_t)(mt_u32(m) >> 5);
   int32_t b = (int32_t)(mt_u32(m) >> 6);
   return (a * 67108864.0 + b) / 9007199254740992.0;
 }
-FFCV_DEV double mt_uniform(DevMT &m, double lo, double hi) {
+FFCV_HD double mt_uniform(DevMT &m, double lo, double hi) {
   double range = hi - lo;
   return lo + range * mt_double(m);
 }
 // legacy RandomState.randint(high): masked rejection on 32-bit draws
-FFCV_DEV int64_t mt_randint(DevMT &m, int64_t high) {
+FFCV_HD int64_t mt_randint(DevMT &m, int64_t high) {
   uint64_t rng = (uint64_t)(high - 1);
   if (rng == 0) return 0;
   uint64_t mask = rng;
@@ -111,14 +149,14 @@ FFCV_DEV int64_t mt_randint(DevMT &m, int64_t high) {
   return (int64_t)v;
 }
 
-FFCV_DEV uint64_t splitmix64(uint64_t x) {
+FFCV_HD uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
 // Seeding contract: op ids 1 = crop, 2 = cutout, 3 = flip.
-FFCV_DEV uint32_t sample_seed(uint64_t loader_seed, uint64_t epoch, uint64_t sample, uint32_t op) {
+FFCV_HD uint32_t sample_seed(uint64_t loader_seed, uint64_t epoch, uint64_t sample, uint32_t op) {
   uint64_t h = splitmix64(loader_seed ^ ((uint64_t)op << 56));
   h = splitmix64(h ^ epoch);
   h = splitmix64(h ^ sample);
@@ -126,7 +164,7 @@ FFCV_DEV uint32_t sample_seed(uint64_t loader_seed, uint64_t epoch, uint64_t sam
 }
 
 // rgb_image.py:48-72 get_random_crop (Python round() = half-to-even = rint)
-FFCV_DEV void random_crop(DevMT &m, uint32_t height, uint32_t width, const double *scale,
+FFCV_HD void random_crop(DevMT &m, uint32_t height, uint32_t width, const double *scale,
                           const double *ratio, int32_t *out) {
   uint32_t area = height * width;
   double lr0 = log(ratio[0]), lr1 = log(ratio[1]);
@@ -165,7 +203,7 @@ FFCV_DEV void random_crop(DevMT &m, uint32_t height, uint32_t width, const doubl
 }
 
 // rgb_image.py:75-81 get_center_crop
-FFCV_DEV void center_crop(uint32_t height, uint32_t width, double ratio, int32_t *out) {
+FFCV_HD void center_crop(uint32_t height, uint32_t width, double ratio, int32_t *out) {
   uint32_t s = height < width ? height : width;
   int64_t c = (int64_t)(ratio * (double)s);
   out[0] = (int32_t)(((int64_t)height - c) / 2);
@@ -178,7 +216,7 @@ FFCV_DEV void center_crop(uint32_t height, uint32_t width, double ratio, int32_t
 // crop (rgb_image.py:48-81) -> crops[4k..], part 1 = cutout origin
 // (cutout.py:38-42) -> cut[2k..], part 2 = flip (flip.py:35) -> flips[k].
 // Returns 1 when the MT19937 stream ran out (FFCV_SAMPLE_RNG).
-FFCV_DEV int draw_part(int part, int k, uint64_t id, uint32_t H, uint32_t W, const ffcv_draw_params &p,
+FFCV_HD int draw_part(int part, int k, uint64_t id, uint32_t H, uint32_t W, const ffcv_draw_params &p,
                        int32_t *crops, int32_t *cut, uint8_t *flips) {
   DevMT m;
   if (part == 0 && crops) {
@@ -229,7 +267,7 @@ struct ResizePlan {
   double scale_x, scale_y, inv_x, inv_y;
 };
 
-FFCV_DEV ResizePlan make_plan(int sw, int sh, int dw, int dh) {
+FFCV_HD ResizePlan make_plan(int sw, int sh, int dw, int dh) {
   ResizePlan p;
   p.sw = sw;
   p.sh = sh;
@@ -258,8 +296,8 @@ FFCV_DEV ResizePlan make_plan(int sw, int sh, int dw, int dh) {
   return p;
 }
 
-FFCV_DEV int sat_u8i(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
-FFCV_DEV int sat_s16i(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+FFCV_HD int sat_u8i(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+FFCV_HD int sat_s16i(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
 
 // computeResizeAreaTab entries for one destination index, as a contiguous
 // source range [lo, hi] with a partial weight at either end (table order is
@@ -270,14 +308,14 @@ struct AreaTaps {
   float wl, wf, wr;
   // s == left ? wl : (s == right ? wr : wf), as register selects (a plain
   // ternary on members becomes a scratch-array lookup)
-  FFCV_DEV float w(int s) const {
-    uint32_t r = __float_as_uint(wf);
-    r = s == right ? __float_as_uint(wr) : r;
-    r = s == left ? __float_as_uint(wl) : r;
-    return __uint_as_float(r);
+  FFCV_HD float w(int s) const {
+    uint32_t r = ffcv_f2u_bits(wf);
+    r = s == right ? ffcv_f2u_bits(wr) : r;
+    r = s == left ? ffcv_f2u_bits(wl) : r;
+    return ffcv_u2f_bits(r);
   }
 };
-FFCV_DEV AreaTaps area_taps(int ssize, double scale, int d) {
+FFCV_HD AreaTaps area_taps(int ssize, double scale, int d) {
   AreaTaps t;
   double fsx1 = d * scale;
   double fsx2 = fsx1 + scale;
@@ -305,7 +343,7 @@ FFCV_DEV AreaTaps area_taps(int ssize, double scale, int d) {
 }
 
 // Linear ("area mode") coefficient for one destination index.
-FFCV_DEV void linear_coef(double scale, double inv, int ssize, int d, int *s_out, int16_t *c0,
+FFCV_HD void linear_coef(double scale, double inv, int ssize, int d, int *s_out, int16_t *c0,
                           int16_t *c1, bool *border) {
   int s = (int)floor(d * scale);
   float f = (float)((d + 1) - (s + 1) * inv);
@@ -320,8 +358,8 @@ FFCV_DEV void linear_coef(double scale, double inv, int ssize, int d, int *s_out
   }
   *s_out = s;
   *border = b;
-  *c0 = (int16_t)sat_s16i(__float2int_rn((1.f - f) * 2048.f));
-  *c1 = (int16_t)sat_s16i(__float2int_rn(f * 2048.f));
+  *c0 = (int16_t)sat_s16i(ffcv_f2i_rn((1.f - f) * 2048.f));
+  *c1 = (int16_t)sat_s16i(ffcv_f2i_rn(f * 2048.f));
 }
 
 // Linear taps of one destination index (linear_coef, precomputable).
@@ -330,7 +368,7 @@ struct LinTap {
   int c0, c1;
   int border;
 };
-FFCV_DEV LinTap lin_tap(double scale, double inv, int ssize, int d) {
+FFCV_HD LinTap lin_tap(double scale, double inv, int ssize, int d) {
   LinTap t;
   int16_t c0, c1;
   bool b;
@@ -345,12 +383,12 @@ FFCV_DEV LinTap lin_tap(double scale, double inv, int ssize, int d) {
 struct RoiSrc {
   const uint8_t *p;
   uint64_t step;  // bytes per row
-  FFCV_DEV int at(int y, int x, int c) const { return p[(uint64_t)y * step + (uint64_t)x * 3 + c]; }
+  FFCV_HD int at(int y, int x, int c) const { return p[(uint64_t)y * step + (uint64_t)x * 3 + c]; }
 };
 
 // INTER_AREA general path for one output pixel from its column/row taps.
 template <class Src>
-FFCV_DEV void resize_area(const Src &S, const AreaTaps &tx, const AreaTaps &ty, int out[3]) {
+FFCV_HD void resize_area(const Src &S, const AreaTaps &tx, const AreaTaps &ty, int out[3]) {
   float sum0 = 0.f, sum1 = 0.f, sum2 = 0.f;
   for (int sy = ty.lo; sy <= ty.hi; sy++) {
     float buf0 = 0.f, buf1 = 0.f, buf2 = 0.f;
@@ -371,15 +409,15 @@ FFCV_DEV void resize_area(const Src &S, const AreaTaps &tx, const AreaTaps &ty, 
       sum2 = sum2 + beta * buf2;
     }
   }
-  out[0] = sat_u8i(__float2int_rn(sum0));
-  out[1] = sat_u8i(__float2int_rn(sum1));
-  out[2] = sat_u8i(__float2int_rn(sum2));
+  out[0] = sat_u8i(ffcv_f2i_rn(sum0));
+  out[1] = sat_u8i(ffcv_f2i_rn(sum1));
+  out[2] = sat_u8i(ffcv_f2i_rn(sum2));
 }
 
 // Area-mode linear (Q11) path for one output pixel; dx is the destination
 // column (the SSE2-body / scalar-tail split depends on it).
 template <class Src>
-FFCV_DEV void resize_linear(const ResizePlan &P, const Src &S, int dx, const LinTap &lx, const LinTap &ly,
+FFCV_HD void resize_linear(const ResizePlan &P, const Src &S, int dx, const LinTap &lx, const LinTap &ly,
                             int out[3]) {
   const int sx = lx.s, sy = ly.s;
   const int r0 = sy < 0 ? 0 : (sy >= P.sh ? P.sh - 1 : sy);
@@ -397,7 +435,7 @@ FFCV_DEV void resize_linear(const ResizePlan &P, const Src &S, int dx, const Lin
     const int e = dx * 3 + c;
     if (e < P.vec_end) {
       int s0 = sat_s16i(h0 >> 4), s1 = sat_s16i(h1 >> 4);
-      int m0 = __mul24(s0, ly.c0) >> 16, m1 = __mul24(s1, ly.c1) >> 16;
+      int m0 = ffcv_mul24(s0, ly.c0) >> 16, m1 = ffcv_mul24(s1, ly.c1) >> 16;
       int t = sat_s16i(m0 + m1);
       out[c] = sat_u8i((t + 2) >> 2);
     } else {
@@ -408,7 +446,7 @@ FFCV_DEV void resize_linear(const ResizePlan &P, const Src &S, int dx, const Lin
 
 // Compute the 3 channels of output pixel (dy, dx).
 template <class Src>
-FFCV_DEV void resize_pixel(const ResizePlan &P, const Src &S, int dy, int dx, int out[3]) {
+FFCV_HD void resize_pixel(const ResizePlan &P, const Src &S, int dy, int dx, int out[3]) {
   if (P.kind == 0) {
     for (int c = 0; c < 3; c++) out[c] = S.at(dy, dx, c);
     return;
@@ -420,7 +458,7 @@ FFCV_DEV void resize_pixel(const ResizePlan &P, const Src &S, int dy, int dx, in
       int sum = 0;
       for (int yy = 0; yy < P.isy; yy++)
         for (int xx = 0; xx < P.isx; xx++) sum += S.at(sy0 + yy, sx0 + xx, c);
-      out[c] = sat_u8i(__float2int_rn((float)sum * sc));
+      out[c] = sat_u8i(ffcv_f2i_rn((float)sum * sc));
     }
     return;
   }
@@ -432,7 +470,7 @@ FFCV_DEV void resize_pixel(const ResizePlan &P, const Src &S, int dy, int dx, in
 }
 
 // Source rows of the crop that output rows [oy0, oy1) read.
-FFCV_DEV void band_rows(const ResizePlan &P, int oy0, int oy1, int *r0, int *r1) {
+FFCV_HD void band_rows(const ResizePlan &P, int oy0, int oy1, int *r0, int *r1) {
   if (P.kind == 0) {
     *r0 = oy0;
     *r1 = oy1 - 1;

@@ -14,8 +14,12 @@ reference, but the decoders run on the HIP device that the Loader feeds:
   needs, resizes with OpenCV INTER_AREA semantics and applies any Cutout /
   RandomHorizontalFlip / NormalizeImage that the graph fused into it.
 
-There is no CPU fallback for JPEG decode or crop-resize: on a machine without
-a HIP device these decoders raise.
+A Loader on ``device='cpu'`` runs the reference's own per-sample host loop
+(rgb_image.py:123-136 / 185-210) against the reference-signature C ABI of
+libffcv_hip.so: ``imdecode`` (executed by the gfx950 JPEG kernels, so JPEG
+still needs the HIP device), ``resize`` (INTER_AREA on the CPU, the kernels'
+own functions) and the contract draws (ffcv_draw_batch_host).  Raw-mode
+datasets therefore load on a CPU-only machine; JPEG raises without a GPU.
 """
 from abc import ABCMeta, abstractmethod
 from dataclasses import replace
@@ -61,12 +65,12 @@ def _pipeline_device(op):
     return getattr(op, '_pipeline_device', None) or ch.device('cpu')
 
 
-def _require_device(op, what):
-    dev = _pipeline_device(op)
-    if dev.type != 'cuda':
-        raise RuntimeError(f'{what} runs on a HIP device (MI355X); this Loader has no GPU. '
-                           'There is no CPU fallback for the decode path.')
-    return dev
+def _host_imdecode(L, data, out, h, w):
+    """libffcv imdecode of one sample into a host buffer; raises on failure
+    (the reference ignores the status, rgb_image.py:131,196)."""
+    if L.imdecode(data, out, h, w, h, w, 0, 0, 1, 1, False, False) != 0:
+        from ..loader.epoch_iterator import DecodeError
+        raise DecodeError('imdecode failed: ' + L.lib().ffcv_last_error().decode(errors='replace'))
 
 
 class SimpleRGBImageDecoder(Operation):
@@ -100,8 +104,6 @@ instead."""
                     (AllocationQuery(biggest_shape, ch.uint8, dev),
                      AllocationQuery((32,), ch.uint8, dev),    # ffcv_sample descriptor
                      AllocationQuery((1,), ch.int32, dev)))    # decode status
-        if self._has_jpg:
-            _require_device(self, 'JPEG decoding')
         self._on_device = False
         my_dtype = np.dtype('<u1')
         return (replace(previous_state, jit_mode=True, shape=biggest_shape, dtype=my_dtype),
@@ -116,7 +118,11 @@ instead."""
                 for dst_ix, source_ix in enumerate(batch_indices):
                     field = metadata[source_ix]
                     image_data = mem_read(field['data_ptr'], storage_state)
-                    L.memcpy(image_data, destination[dst_ix])
+                    if field['mode'] == IMAGE_MODES['jpg']:
+                        _host_imdecode(L, image_data, destination[dst_ix], int(field['height']),
+                                       int(field['width']))
+                    else:
+                        L.memcpy(image_data, destination[dst_ix])
                 return destination[:len(batch_indices)]
             return decode_host
 
@@ -167,8 +173,14 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
         heights = self.metadata['height']
         self.max_width = np.uint64(widths.max())
         self.max_height = np.uint64(heights.max())
-        dev = _require_device(self, type(self).__name__)
+        dev = _pipeline_device(self)
         output_shape = (int(self.output_size[0]), int(self.output_size[1]), 3)
+        self._on_device = dev.type == 'cuda'
+        if not self._on_device:  # rgb_image.py:151-166: output + full-image temp per sample
+            u1 = np.dtype('<u1')
+            return (replace(previous_state, jit_mode=True, shape=output_shape, dtype=u1),
+                    (AllocationQuery(output_shape, u1),
+                     AllocationQuery((int(self.max_height) * int(self.max_width) * 3,), u1)))
         return (
             replace(previous_state, jit_mode=False, device=dev, shape=output_shape,
                     dtype=self.output_dtype),
@@ -206,8 +218,55 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
         p.epoch = int(ss.epoch)
         return p
 
+    def _generate_code_host(self) -> Callable:
+        """The reference's per-sample loop (rgb_image.py:185-210) on host
+        buffers through the C ABI (imdecode / draws / resize)."""
+        from .. import libffcv as L
+        from ..pipeline import runtime
+        mem_read = self.memory_read
+        jpg = IMAGE_MODES['jpg']
+
+        def decode(batch_indices, my_storage, metadata, storage_state):
+            destination, temp_storage = my_storage
+            B = len(batch_indices)
+            ids = np.asarray(batch_indices, dtype=np.uint64)
+            fields = metadata[ids.astype(np.int64)]
+            ctx = runtime.current()
+            seed, epoch = (ctx.loader_seed, ctx.epoch) if ctx is not None else (0, 0)
+            out_h, out_w = int(destination.shape[1]), int(destination.shape[2])
+            dp = self._make_draw_params_seed(seed, epoch, out_h, out_w)
+            crops = np.empty((B, 4), np.int32)
+            L.draw_batch_host(ids, fields['height'], fields['width'], dp, crops)
+            for k in range(B):
+                field = fields[k]
+                h, w = int(field['height']), int(field['width'])
+                image_data = mem_read(field['data_ptr'], storage_state)
+                if field['mode'] == jpg:
+                    buf = temp_storage[k][:h * w * 3]
+                    _host_imdecode(L, image_data, buf, h, w)
+                    img = buf.reshape(h, w, 3)
+                else:
+                    img = image_data.reshape(h, w, 3)
+                i, j, ch_, cw = (int(x) for x in crops[k])
+                L.resize_crop(img, i, i + ch_, j, j + cw, destination[k])
+            return destination[:B]
+        decode.is_parallel = True
+        return decode
+
+    def _make_draw_params_seed(self, seed, epoch, out_h, out_w):
+        class _S:
+            pass
+        ss = _S()
+        ss.loader_seed, ss.epoch = seed, epoch
+        p = self._make_draw_params(ss, out_h, out_w)
+        p.cutout_size = 0  # host Cutout / flip run as their own operations
+        p.flip_prob = 0.0
+        return p
+
     def generate_code(self) -> Callable:
         from .. import libffcv as L
+        if not getattr(self, '_on_device', True):
+            return self._generate_code_host()
         f_ix = self._field_index
         rp = L.RRCParams()
         cut = self._fused_cutout

@@ -73,9 +73,14 @@ _SIGS = {
     'ffcv_memcpy_h2d_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     'ffcv_memcpy_d2h_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     'my_memcpy': (None, [c_void_p, c_void_p, c_uint64]),
+    'resize': (None, [ctypes.c_int64] * 11),
+    'imdecode': (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32,
+                         c_uint32, c_uint32, c_uint32, c_uint32, ctypes.c_bool, ctypes.c_bool]),
     'ffcv_host_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int]),
     'ffcv_draw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
+    'ffcv_draw_batch_host': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
     'ffcv_rrc_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
     'ffcv_gather_samples': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_int, c_void_p]),
@@ -173,6 +178,48 @@ def memcpy(source: np.ndarray, dest: np.ndarray):
     lib().my_memcpy(source.ctypes.data, dest.ctypes.data, source.size * source.itemsize)
 
 
+# --------------------------------------- reference one-sample host API --
+# ffcv/libffcv.py:11-48: read (libc pread), resize_crop, imdecode, same
+# names and argument meaning, for Operations written against the reference.
+_libc = None
+
+
+def read(fileno: int, destination: np.ndarray, offset: int):
+    """pread(fileno, destination, destination.size, offset) (libffcv.py:11-19)."""
+    global _libc
+    if _libc is None:
+        _libc = ctypes.CDLL('libc.so.6', use_errno=True)
+        _libc.pread.restype = ctypes.c_ssize_t
+        _libc.pread.argtypes = [c_int, c_void_p, ctypes.c_size_t, ctypes.c_int64]
+    return _libc.pread(int(fileno), destination.ctypes.data, destination.size, int(offset))
+
+
+def resize_crop(source, start_row, end_row, start_col, end_col, destination):
+    """INTER_AREA resize of source[start_row:end_row, start_col:end_col]
+    (HWC uint8) into destination (its shape is the target), libffcv.py:22-31."""
+    source = np.asarray(source)
+    if source.dtype != np.uint8 or destination.dtype != np.uint8 or not source.flags.c_contiguous \
+            or not destination.flags.c_contiguous:
+        raise ValueError('resize_crop: source and destination must be C-contiguous uint8 HWC arrays')
+    lib().resize(0, source.ctypes.data, source.shape[0], source.shape[1], int(start_row), int(end_row),
+                 int(start_col), int(end_col), destination.ctypes.data, destination.shape[0],
+                 destination.shape[1])
+
+
+def imdecode(source: np.ndarray, dst: np.ndarray, source_height: int, source_width: int,
+             crop_height=None, crop_width=None, offset_x=0, offset_y=0, scale_factor_num=1,
+             scale_factor_denom=1, enable_crop=False, do_flip=False):
+    """Decode one JPEG (host bytes) into dst (host HWC uint8), libffcv.py:34-48;
+    runs on the HIP device.  Returns 0 or -1 like tjDecompress2."""
+    if crop_height is None:
+        crop_height = source_height
+    if crop_width is None:
+        crop_width = source_width
+    return lib().imdecode(source.ctypes.data, source.size, int(source_height), int(source_width),
+                          dst.ctypes.data, int(crop_height), int(crop_width), int(offset_x), int(offset_y),
+                          int(scale_factor_num), int(scale_factor_denom), bool(enable_crop), bool(do_flip))
+
+
 def host_gather(src: np.ndarray, src_off: np.ndarray, sizes: np.ndarray, dst_off: np.ndarray, dst,
                 nthreads=8):
     """Gather byte ranges of a host buffer (e.g. the mmap) into dst (numpy / pinned tensor)."""
@@ -188,6 +235,15 @@ def draw_batch(ids, samples, params: DrawParams, crops=None, cutout_yx=None, fli
     _check(lib().ffcv_draw_batch(_stream(stream), _p(ids), _p(samples), int(ids.shape[0]),
                                  ctypes.byref(params), _p(crops), _p(cutout_yx), _p(flips),
                                  _p(status)), 'ffcv_draw_batch')
+
+
+def draw_batch_host(ids, heights, widths, params: DrawParams, crops=None, cutout_yx=None, flips=None):
+    """ffcv_draw_batch on host arrays (the CPU-device decoders' draws)."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    hs = np.ascontiguousarray(heights, dtype=np.uint32) if heights is not None else None
+    ws = np.ascontiguousarray(widths, dtype=np.uint32) if widths is not None else None
+    _check(lib().ffcv_draw_batch_host(_p(ids), _p(hs), _p(ws), int(ids.size), ctypes.byref(params), _p(crops),
+                                      _p(cutout_yx), _p(flips)), 'ffcv_draw_batch_host')
 
 
 def gather_samples(table, ids, out, stream=None):

@@ -24,6 +24,7 @@
  */
 #ifndef FFCV_HIP_H
 #define FFCV_HIP_H
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -110,6 +111,29 @@ int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stre
  * CPU-only Loader, C1).  Same argument order as the reference. */
 void my_memcpy(void *source, void *dst, uint64_t size);
 
+/* libffcv.cpp:33-42 resize: cv::resize(src[start_row:end_row,
+ * start_col:end_col], dst, (tx rows, ty cols), INTER_AREA) where src is an
+ * sx x sy x 3 uint8 image and dst a tx x ty x 3 uint8 buffer, both in host
+ * memory (bound as resize_crop, ffcv/libffcv.py:22-31; cresizer unused).
+ * Computed on the CPU by the kernels' own INTER_AREA functions.  On an
+ * invalid ROI nothing is written and ffcv_last_error() says why. */
+void resize(int64_t cresizer, int64_t source_p, int64_t sx, int64_t sy,
+            int64_t start_row, int64_t end_row, int64_t start_col,
+            int64_t end_col, int64_t dest_p, int64_t tx, int64_t ty);
+
+/* libffcv.cpp:53-112 imdecode (bound at ffcv/libffcv.py:34-48): decode the
+ * JPEG input_buffer[input_size] to crop_height x crop_width x 3 RGB in host
+ * output_buffer, tjDecompress2(TJPF_RGB, TJFLAG_FASTDCT) semantics, on the
+ * HIP device (per-thread stream and decoder context).  Returns 0, or -1 on a
+ * decode error / size mismatch / when enable_crop, hflip or a scale other
+ * than 1 is requested (never used by ffcv) -- see ffcv_last_error(). */
+int imdecode(unsigned char *input_buffer, uint64_t input_size,
+             uint32_t source_height, uint32_t source_width,
+             unsigned char *output_buffer, uint32_t crop_height,
+             uint32_t crop_width, uint32_t offset_x, uint32_t offset_y,
+             uint32_t scale_num, uint32_t scale_denom, bool enable_crop,
+             bool hflip);
+
 /* Host gather of n byte ranges src + src_off[i] (sizes[i] bytes) to
  * dst + dst_off[i], split over nthreads threads by bytes: the PCIe path's
  * per-batch staging of compressed samples from the mmap'd .beton
@@ -131,6 +155,13 @@ int ffcv_draw_batch(void *stream, const uint64_t *sample_ids,
                     const ffcv_sample *samples, int batch,
                     const ffcv_draw_params *p, int32_t *crops,
                     int32_t *cutout_yx, uint8_t *flips, int32_t *status);
+
+/* The same draws on the host (the CPU-device Loader's decoders): heights /
+ * widths / sample_ids are host arrays, outputs host arrays. */
+int ffcv_draw_batch_host(const uint64_t *sample_ids, const uint32_t *heights,
+                         const uint32_t *widths, int batch,
+                         const ffcv_draw_params *p, int32_t *crops,
+                         int32_t *cutout_yx, uint8_t *flips);
 
 /* ------------------------------------------- raw-mode crop + resize ---- */
 /* rgb_image.py:202-208 (raw branch) + libffcv.cpp:33-42 cv::resize

@@ -432,3 +432,38 @@ def test_jpeg_rrc_fused_matches_staged(hip_lib, oracle):
         want = oracle.rrc_batch([(blobs[i], hs[i], ws[i], 0)], crops[k:k + 1], 224, 224)
         want = _oracle_post(want, flips[k:k + 1], cut[k:k + 1], 32, (124, 116, 103))
         assert np.array_equal(res[1][4][k], want[0]), k
+
+
+def test_host_imdecode_matches_libjpeg(hip_lib, oracle):
+    """libffcv.cpp:53-112 imdecode (reference signature, host buffers in and
+    out) executed by the gfx950 kernels: bit-exact with libjpeg-turbo ifast
+    + fancy on mixed subsampling / quality / greyscale / odd sizes, from
+    several host threads at once (per-thread stream + decoder context), and
+    -1 on a corrupt stream or a size mismatch."""
+    _torch()
+    import threading
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(31)
+    imgs, blobs = _jpeg_set(rng, 24, max_side=300)
+    want = [oracle.ljt_decode(b) for b in blobs]
+    errors = []
+
+    def work(ks):
+        for k in ks:
+            h, w = imgs[k].shape[:2]
+            out = np.zeros((h, w, 3), np.uint8)
+            rc = L.imdecode(blobs[k], out, h, w, h, w, 0, 0, 1, 1, False, False)
+            if rc != 0 or not np.array_equal(out, want[k]):
+                errors.append((k, rc))
+    ths = [threading.Thread(target=work, args=(range(t, 24, 4),)) for t in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    h, w = imgs[0].shape[:2]
+    out = np.zeros((h, w, 3), np.uint8)
+    bad = blobs[0].copy()
+    bad[:2] = 0  # no SOI
+    assert L.imdecode(bad, out, h, w, h, w) == -1
+    assert L.imdecode(blobs[0], np.zeros((h + 1, w, 3), np.uint8), h + 1, w, h + 1, w) == -1

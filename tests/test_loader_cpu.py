@@ -86,11 +86,63 @@ def test_host_transforms_follow_contract(raw_beton):
         assert np.array_equal(im[k], want)
 
 
-def test_decode_path_requires_gpu(tmp_path):
+def test_cpu_device_rrc_raw_matches_oracle(tmp_path, oracle):
+    """device='cpu' RRC on a raw .beton runs the reference's per-sample host
+    loop (rgb_image.py:185-210) through the C ABI (ffcv_draw_batch_host +
+    resize); with host Cutout / flip / NormalizeImage after it, bit-exact
+    against the oracle under the seeding contract."""
+    from tests.helpers import samples_of, expected_rrc
+    fn = write(str(tmp_path / 'nat_raw.beton'), NaturalDS(40, hw=(90, 70), var=True, seed=3),
+               {'image': RGBImageField(write_mode='raw'), 'label': IntField()})
+    samples = samples_of(fn)
+    mean, std = np.array([120., 110., 100.]), np.array([60., 55., 50.])
+    lut = oracle.normalize_lut(mean, std)
+    loader = Loader(fn, batch_size=8, seed=6, order=OrderOption.RANDOM, device='cpu', pipelines={
+        'image': [RandomResizedCropRGBImageDecoder((48, 40)), Cutout(9, (1, 2, 3)), RandomHorizontalFlip(0.5),
+                  NormalizeImage(mean, std, np.float16), ToTensor()]})
+    for epoch in range(2):
+        order = np.random.default_rng(6 + epoch).permutation(40)
+        for b, (images, labels) in enumerate(loader):
+            ids = order[b * 8:(b + 1) * 8]
+            want = expected_rrc(oracle, samples, ids, 6, epoch, (48, 40), cutout=9, fill=(1, 2, 3),
+                                flip_p=0.5, cut_before_flip=True, lut=lut)
+            assert np.array_equal(images.numpy().view(np.uint16), want.view(np.uint16))
+            assert (labels.numpy().reshape(-1) == ids % 10).all()
+
+
+def test_host_draws_match_oracle(oracle):
+    """ffcv_draw_batch_host (the device draw functions compiled for the host)
+    equals the oracle's draws, crop / center crop / cutout."""
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(1)
+    n = 3000
+    ids = rng.integers(0, 2 ** 40, n).astype(np.uint64)
+    hs = rng.integers(1, 700, n).astype(np.uint32)
+    ws = rng.integers(1, 700, n).astype(np.uint32)
+    for kind in (0, 1):
+        p = L.DrawParams()
+        p.crop_kind, p.out_h, p.out_w, p.cutout_size = kind, 224, 224, 32
+        p.scale[0], p.scale[1] = 0.08, 1.0
+        p.ratio[0], p.ratio[1] = 0.75, 4 / 3
+        p.center_ratio = 224 / 256
+        p.loader_seed, p.epoch = 12345, 7
+        crops = np.zeros((n, 4), np.int32)
+        cut = np.zeros((n, 2), np.int32)
+        L.draw_batch_host(ids, hs, ws, p, crops, cut)
+        oc, ocut = oracle.draw_batch(ids, hs, ws, 12345, 7, crop='random' if kind == 0 else 'center',
+                                     cutout_size=32)
+        assert np.array_equal(crops, oc) and np.array_equal(cut, ocut)
+
+
+def test_cpu_device_jpeg_needs_the_hip_device(tmp_path):
+    """JPEG on device='cpu' decodes through imdecode, which runs on the HIP
+    device: without one it fails loudly (no CPU JPEG decoder in the product)."""
+    if ch.cuda.is_available():
+        pytest.skip('covered by the GPU test of the same path')
+    from ffcv_amd.loader.epoch_iterator import DecodeError
     fn = write(str(tmp_path / 'j.beton'), NaturalDS(8), {'image': RGBImageField(write_mode='jpg'),
                                                           'label': IntField()})
-    with pytest.raises(RuntimeError, match='HIP device'):
-        Loader(fn, batch_size=4, device='cpu')
-    with pytest.raises(RuntimeError, match='HIP device'):
-        Loader(fn, batch_size=4, device='cpu',
-               pipelines={'image': [RandomResizedCropRGBImageDecoder((32, 32))]})
+    for pipe in (None, [RandomResizedCropRGBImageDecoder((32, 32)), ToTensor()]):
+        loader = Loader(fn, batch_size=4, device='cpu', pipelines={'image': pipe} if pipe else {})
+        with pytest.raises(DecodeError, match='imdecode'):
+            next(iter(loader))

@@ -22,7 +22,7 @@ from ffcv_amd.fields.decoders import (RandomResizedCropRGBImageDecoder, CenterCr
 from ffcv_amd.transforms import (ToTensor, ToDevice, ToTorchImage, NormalizeImage, Cutout,
                                  RandomHorizontalFlip, Convert)
 from ffcv_amd.loader.epoch_iterator import DecodeError
-from tests.helpers import ConstDS, NaturalDS, write
+from tests.helpers import ConstDS, NaturalDS, write, samples_of as _samples, expected_rrc as _expected
 
 pytestmark = pytest.mark.gpu
 MEAN = np.array([0.485, 0.456, 0.406]) * 255
@@ -38,40 +38,6 @@ def need_gpu(hip_lib):
 @pytest.fixture(scope='module')
 def tmpdir_m():
     return tempfile.mkdtemp()
-
-
-def _samples(fn):
-    r = Reader(fn)
-    mm = np.memmap(fn, np.uint8, mode='r')
-    sizes = dict(zip(r.alloc_table['ptr'].tolist(), r.alloc_table['size'].tolist()))
-    out = []
-    for md in r.metadata['f0']:
-        p = int(md['data_ptr'])
-        out.append((np.array(mm[p:p + sizes[p]]), int(md['height']), int(md['width']), int(md['mode'])))
-    return out
-
-
-def _expected(oracle, samples, ids, seed, epoch, out_hw, crop='random', ratio=224 / 256,
-              cutout=0, fill=(0, 0, 0), flip_p=0.0, cut_before_flip=False, lut=None):
-    ids = np.asarray(ids, np.uint64)
-    hs = [samples[int(i)][1] for i in ids]
-    ws = [samples[int(i)][2] for i in ids]
-    crops, cyx = oracle.draw_batch(ids, hs, ws, seed, epoch, crop=crop, center_ratio=ratio,
-                                   out_h=out_hw[0], out_w=out_hw[1], cutout_size=cutout)
-    u8 = oracle.rrc_batch([samples[int(i)] for i in ids], crops, out_hw[0], out_hw[1])
-    for k, sid in enumerate(ids):
-        if cutout and cut_before_flip:
-            y, x = cyx[k]
-            u8[k, y:y + cutout, x:x + cutout] = fill
-        if flip_p and oracle.MT(oracle.sample_seed(seed, epoch, int(sid), 3)).uniform(0, 1) < flip_p:
-            u8[k] = u8[k, :, ::-1]
-        if cutout and not cut_before_flip:
-            y, x = cyx[k]
-            u8[k, y:y + cutout, x:x + cutout] = fill
-    if lut is not None:
-        idx = u8.astype(np.int64)
-        return np.stack([lut[idx[..., c], c] for c in range(3)], -1)
-    return u8
 
 
 @pytest.mark.parametrize('mode', ['raw', 'jpg'])
@@ -388,3 +354,30 @@ def test_early_break_then_next_epoch(tmpdir_m, oracle):
             if epoch == 1 and b == 4:
                 break  # abandon again mid-epoch
         assert n == (5 if epoch == 1 else 10)
+
+
+def test_cpu_device_loader_jpeg(tmpdir_m, oracle):
+    """device='cpu' on a JPEG .beton: the reference's host loop through the
+    reference-signature C ABI (imdecode on the HIP device, host draws and
+    INTER_AREA resize), host tensors out, bit-exact against the oracle; and
+    the default Simple pipeline on constant-size JPEGs."""
+    fn = os.path.join(tmpdir_m, 'cpu_jpg.beton')
+    write(fn, NaturalDS(40, hw=(90, 110), var=True, seed=12),
+          {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    samples = _samples(fn)
+    loader = Loader(fn, batch_size=8, seed=5, order=OrderOption.RANDOM, device='cpu',
+                    pipelines={'image': [RandomResizedCropRGBImageDecoder((56, 48)), Cutout(7, (9, 8, 7)),
+                                         ToTensor()]})
+    order = np.random.default_rng(5).permutation(40)
+    for b, (images, labels) in enumerate(loader):
+        assert images.device.type == 'cpu'
+        ids = order[b * 8:(b + 1) * 8]
+        want = _expected(oracle, samples, ids, 5, 0, (56, 48), cutout=7, fill=(9, 8, 7), cut_before_flip=True)
+        assert np.array_equal(images.numpy(), want)
+    fn2 = os.path.join(tmpdir_m, 'cpu_jpg_const.beton')
+    write(fn2, NaturalDS(12, hw=(40, 56), seed=13), {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    s2 = _samples(fn2)
+    for images, labels in Loader(fn2, batch_size=4, device='cpu'):
+        for k in range(4):
+            i = int(np.nonzero([np.array_equal(oracle.jpeg_decode(s[0]), images[k].numpy()) for s in s2])[0][0])
+            assert int(labels[k]) == i % 10

@@ -282,6 +282,47 @@ def gen_betons(ffcv):
     return out
 
 
+def gen_quasi():
+    """QuasiRandom orders (quasi_random.py:14-85) on a multi-page .beton
+    written by the reference writer: the allocation table (which defines the
+    page -> sample sets) and the orders for several seeds / batch sizes /
+    index subsets / epochs."""
+    from ffcv.writer import DatasetWriter
+    from ffcv.fields import RGBImageField, IntField
+    from ffcv.reader import Reader
+    from ffcv.memory_managers import OSCacheManager
+    from ffcv.traversal_order.quasi_random import QuasiRandom
+    out = {}
+
+    class FakeLoader:
+        pass
+    with tempfile.TemporaryDirectory() as d:
+        fn = os.path.join(d, 'quasi.beton')
+        w = DatasetWriter(fn, {'image': RGBImageField(write_mode='raw'), 'label': IntField()},
+                          page_size=1 << 21, num_workers=1)
+        w.from_indexed_dataset(_RawDS(300, [(60, 80), (100, 120), (30, 40), (90, 70)], 7), chunksize=10)
+        r = Reader(fn)
+        at = r.alloc_table
+        out['alloc'] = np.stack([at['sample_id'].astype(np.int64), at['ptr'].astype(np.int64),
+                                 at['size'].astype(np.int64)], 1)
+        out['page_size'] = np.array([r.page_size], np.int64)
+        mm = OSCacheManager(r)
+        for seed in [0, 7, 4000]:
+            for bs in [4, 16]:
+                for kind in ['all', 'third']:
+                    fl = FakeLoader()
+                    fl.memory_manager = mm
+                    fl.indices = np.arange(300, dtype='uint64') if kind == 'all' else \
+                        np.arange(0, 300, 3, dtype='uint64')
+                    fl.seed = seed
+                    fl.distributed = False
+                    fl.batch_size = bs
+                    q = QuasiRandom(fl)
+                    for epoch in [0, 1, 3]:
+                        out[f'order_s{seed}_b{bs}_{kind}_e{epoch}'] = np.asarray(q.sample_order(epoch), np.int64)
+    return out
+
+
 def main():
     install_stubs()
     sys.path.insert(0, REF)
@@ -298,6 +339,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, 'normalize_lut.npz'), **gen_lut(NormalizeImage))
     np.savez_compressed(os.path.join(HERE, 'orders.npz'), **gen_orders(Random, Sequential))
     np.savez_compressed(os.path.join(HERE, 'betons.npz'), **gen_betons(ffcv))
+    np.savez_compressed(os.path.join(HERE, 'quasi.npz'), **gen_quasi())
     print('golden vectors written to', HERE)
 
 

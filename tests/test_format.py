@@ -69,12 +69,16 @@ def test_reader_parses_reference_files(name):
                 assert np.array_equal(mm[md['data_ptr']:md['data_ptr'] + size], img.reshape(-1))
 
 
-@pytest.mark.parametrize('name', ['raw32', 'rawvar', 'jpgvar'])
-def test_writer_reproduces_reference_bytes(name):
+@pytest.mark.parametrize('name', ['raw32', 'rawvar', 'jpgvar', 'smart_maxres'])
+def test_writer_reproduces_reference_bytes(name, hip_lib):
+    """DatasetWriter output == the reference writer's file, byte for byte;
+    smart_maxres runs the max_resolution INTER_AREA shrink (rgb_image.py:37-45)
+    through the host C-ABI resize and the smart raw/jpg choice."""
     g = np.load(os.path.join(GOLD, 'betons.npz'))
     n, seed, shapes = _spec(g, name)
     kw = {'raw32': dict(write_mode='raw'), 'rawvar': dict(write_mode='raw'),
-          'jpgvar': dict(write_mode='jpg', jpeg_quality=90)}[name]
+          'jpgvar': dict(write_mode='jpg', jpeg_quality=90),
+          'smart_maxres': dict(write_mode='smart', max_resolution=48, smart_threshold=3000)}[name]
     with tempfile.TemporaryDirectory() as d:
         fn = os.path.join(d, 'x.beton')
         DatasetWriter(fn, {'image': RGBImageField(**kw), 'label': IntField()},

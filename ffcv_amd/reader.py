@@ -1,5 +1,18 @@
-"""``.beton`` reader (ffcv/reader.py:7-72): header, field descriptors,
-per-sample metadata (structured dtype) and the allocation table."""
+"""``.beton`` reader.
+
+File layout (format version 2; reference parser
+ffcv/reader.py:7-72):
+
+    [ header: HeaderType, 24 B ]
+    [ num_fields x FieldDescType (type id, name, 1024-byte argument blob) ]
+    [ num_samples x metadata record (one struct member per field) ]
+    [ data pages ... ]
+    [ allocation table (sample_id, ptr, size) x n at header.alloc_table_ptr ]
+
+Everything is parsed with ``np.fromfile`` into read-only structured arrays;
+sample bytes themselves are left to the memory managers (mmap / page cache)
+and, on the device path, to the HBM copy of the whole file.
+"""
 import numpy as np
 
 from .utils import decode_null_terminated_string
@@ -7,11 +20,21 @@ from .types import (ALLOC_TABLE_TYPE, HeaderType, CURRENT_VERSION, FieldDescType
                     get_handlers, get_metadata_type)
 
 
+def _frozen(a):
+    a.setflags(write=False)
+    return a
+
+
 class Reader:
+    """Parsed header, field handlers, metadata and allocation table of one file.
+
+    ``custom_handlers`` maps a field name to the Field class of a custom
+    (type id 255) field, whose descriptor cannot name its own handler.
+    """
 
     def __init__(self, fname, custom_handlers={}):
         self._fname = fname
-        self._custom_handlers = custom_handlers
+        self._custom_handlers = dict(custom_handlers)
         self.read_header()
         self.read_field_descriptors()
         self.read_metadata()
@@ -22,42 +45,34 @@ class Reader:
         return self._fname
 
     def read_header(self):
-        header = np.fromfile(self._fname, dtype=HeaderType, count=1)[0]
-        header.setflags(write=False)
-        version = header['version']
-        if version != CURRENT_VERSION:
-            raise AssertionError(f"file format mismatch: code={CURRENT_VERSION},file={version}")
-        self.num_samples = header['num_samples']
-        self.page_size = header['page_size']
-        self.num_fields = header['num_fields']
-        self.header = header
+        self.header = _frozen(np.fromfile(self._fname, dtype=HeaderType, count=1))[0]
+        if self.header['version'] != CURRENT_VERSION:
+            raise AssertionError(f"file format mismatch: code={CURRENT_VERSION},"
+                                 f"file={self.header['version']}")
+        self.num_samples = self.header['num_samples']
+        self.page_size = self.header['page_size']
+        self.num_fields = self.header['num_fields']
 
     def read_field_descriptors(self):
-        offset = HeaderType.itemsize
-        field_descriptors = np.fromfile(self._fname, dtype=FieldDescType, count=self.num_fields,
-                                        offset=offset)
-        field_descriptors.setflags(write=False)
-        handlers = get_handlers(field_descriptors)
-        self.field_descriptors = field_descriptors
-        self.field_names = list(map(decode_null_terminated_string, self.field_descriptors['name']))
-        self.handlers = dict(zip(self.field_names, handlers))
-        for field_name, field_desc in zip(self.field_names, self.field_descriptors):
-            if field_name in self._custom_handlers:
-                CustomHandler = self._custom_handlers[field_name]
-                self.handlers[field_name] = CustomHandler.from_binary(field_desc['arguments'])
-        for field_name, handler in self.handlers.items():
+        descs = _frozen(np.fromfile(self._fname, dtype=FieldDescType, count=self.num_fields,
+                                    offset=HeaderType.itemsize))
+        self.field_descriptors = descs
+        self.field_names = [decode_null_terminated_string(d['name']) for d in descs]
+        handlers = {}
+        for name, desc, builtin in zip(self.field_names, descs, get_handlers(descs)):
+            custom = self._custom_handlers.get(name)
+            handler = custom.from_binary(desc['arguments']) if custom is not None else builtin
             if handler is None:
-                raise ValueError(f"Must specify a custom_field entry for custom field {field_name}")
-        self.metadata_type = get_metadata_type(list(self.handlers.values()))
+                raise ValueError(f"Must specify a custom_field entry for custom field {name}")
+            handlers[name] = handler
+        self.handlers = handlers
+        self.metadata_type = get_metadata_type(list(handlers.values()))
 
     def read_metadata(self):
-        offset = HeaderType.itemsize + self.field_descriptors.nbytes
-        self.metadata = np.fromfile(self._fname, dtype=self.metadata_type, count=self.num_samples,
-                                    offset=offset)
-        self.metadata.setflags(write=False)
+        start = HeaderType.itemsize + self.field_descriptors.nbytes
+        self.metadata = _frozen(np.fromfile(self._fname, dtype=self.metadata_type,
+                                            count=self.num_samples, offset=start))
 
     def read_allocation_table(self):
-        offset = self.header['alloc_table_ptr']
-        alloc_table = np.fromfile(self._fname, dtype=ALLOC_TABLE_TYPE, offset=offset)
-        alloc_table.setflags(write=False)
-        self.alloc_table = alloc_table
+        self.alloc_table = _frozen(np.fromfile(self._fname, dtype=ALLOC_TABLE_TYPE,
+                                               offset=self.header['alloc_table_ptr']))

@@ -1,10 +1,11 @@
-"""General operations (ffcv/transforms/ops.py:17-160): ToTensor, ToDevice,
-ToTorchImage, Convert, View.
+"""Layout / placement operations: ToTensor, ToDevice, ToTorchImage, Convert, View.
 
-Device stages hand tensors between kernels on the slot's HIP stream.
-``ToTensor`` and ``ToDevice`` are free when the decoder already produced a
-tensor on the target device (the device-resident path); otherwise they do
-exactly what the reference does (from_numpy / non_blocking H2D copy).
+Semantics of the reference's ffcv/transforms/ops.py:17-160.  On the
+device-resident path they are mostly free: the decode launch already wrote a
+tensor on the Loader's device, so ToTensor / ToDevice pass it through and
+ToTorchImage only re-labels the channels-last storage as NCHW.  On host data
+they do what the reference does (``torch.from_numpy``, a non_blocking copy
+into the slot's device buffer, an NCHW view or copy).
 """
 from dataclasses import replace
 from typing import Callable, Optional, Tuple
@@ -17,14 +18,18 @@ from ..pipeline.operation import Operation
 from ..pipeline.state import State
 
 
-def _torch_dtype(dtype):
-    if isinstance(dtype, ch.dtype):
-        return dtype
-    return ch.from_numpy(np.empty((), dtype=dtype)).dtype
+def _as_torch_dtype(dtype):
+    return dtype if isinstance(dtype, ch.dtype) else ch.from_numpy(np.empty((), dtype=dtype)).dtype
+
+
+def _same_device(state_device, target):
+    """True when data on ``state_device`` already satisfies ``ToDevice(target)``
+    (an index-less 'cuda' target accepts any GPU)."""
+    return state_device.type == target.type and (target.index is None or state_device == target)
 
 
 class ToTensor(Operation):
-    """Convert from Numpy array to PyTorch Tensor."""
+    """numpy batch -> torch tensor (zero copy); tensors pass through."""
     device_aware = True
     per_sample = True
 
@@ -33,18 +38,15 @@ class ToTensor(Operation):
 
     def generate_code(self) -> Callable:
         def to_tensor(inp, dst):
-            if isinstance(inp, ch.Tensor):
-                return inp
-            return ch.from_numpy(inp)
+            return inp if isinstance(inp, ch.Tensor) else ch.from_numpy(inp)
         return to_tensor
 
     def declare_state_and_memory(self, previous_state: State) -> Tuple[State, Optional[AllocationQuery]]:
-        new_dtype = _torch_dtype(previous_state.dtype)
-        return replace(previous_state, jit_mode=False, dtype=new_dtype), None
+        return replace(previous_state, jit_mode=False, dtype=_as_torch_dtype(previous_state.dtype)), None
 
 
 class ToDevice(Operation):
-    """Move tensor to device (ops.py:32-62).
+    """Move the batch to ``device`` (asynchronous when ``non_blocking``).
 
     Parameters
     ----------
@@ -63,39 +65,38 @@ class ToDevice(Operation):
 
     def generate_code(self) -> Callable:
         target = ch.device(self.device)
+        non_blocking = self.non_blocking
 
         def to_device(inp, dst):
-            if inp.device == target or (target.type == inp.device.type == 'cuda' and
-                                        target.index is None):
+            if _same_device(inp.device, target):
                 return inp
-            if len(inp.shape) == 4:
-                if inp.is_contiguous(memory_format=ch.channels_last):
-                    dst = dst.reshape(inp.shape[0], inp.shape[2], inp.shape[3], inp.shape[1])
-                    dst = dst.permute(0, 3, 1, 2)
-            dst = dst[:inp.shape[0]]
-            dst.copy_(inp, non_blocking=self.non_blocking)
-            return dst
+            n = inp.shape[0]
+            if inp.dim() == 4 and inp.is_contiguous(memory_format=ch.channels_last):
+                # keep the channels-last storage order of an NCHW view
+                b, c, h, w = inp.shape
+                dst = dst.reshape(dst.shape[0], h, w, c).permute(0, 3, 1, 2)
+            out = dst[:n]
+            out.copy_(inp, non_blocking=non_blocking)
+            return out
         return to_device
 
     def declare_state_and_memory(self, previous_state: State) -> Tuple[State, Optional[AllocationQuery]]:
         target = ch.device(self.device)
-        if previous_state.device.type == target.type and (target.index is None or
-                                                          previous_state.device == target):
-            return replace(previous_state, device=previous_state.device), None
-        return replace(previous_state, device=target), AllocationQuery(previous_state.shape,
-                                                                       dtype=previous_state.dtype,
-                                                                       device=target)
+        if _same_device(previous_state.device, target):
+            return previous_state, None
+        buffer = AllocationQuery(previous_state.shape, dtype=previous_state.dtype, device=target)
+        return replace(previous_state, device=target), buffer
 
 
 class ToTorchImage(Operation):
-    """Change tensor to PyTorch format for images (B x C x H x W).
+    """NHWC batch -> NCHW (B x C x H x W) as torch expects images.
 
     Parameters
     ----------
     channels_last : bool
-        Use torch.channels_last.
+        Use torch.channels_last (a permuted view, no copy).
     convert_back_int16 : bool
-        Convert to float16.
+        Reinterpret int16 storage (NormalizeImage's fp16 bits) as float16.
     """
     device_aware = True
     per_sample = True
@@ -107,34 +108,34 @@ class ToTorchImage(Operation):
         self.enable_int16conv = False
 
     def generate_code(self) -> Callable:
-        do_conv = self.enable_int16conv
-        channels_last = self.channels_last
+        as_fp16 = self.enable_int16conv
+        keep_view = self.channels_last
 
         def to_torch_image(inp: ch.Tensor, dst):
-            if do_conv:
+            if as_fp16:
                 inp = inp.view(dtype=ch.float16)
-            inp = inp.permute([0, 3, 1, 2])
-            if channels_last:
-                assert inp.is_contiguous(memory_format=ch.channels_last)
-                return inp
-            dst[:inp.shape[0]] = inp.contiguous()
-            return dst[:inp.shape[0]]
+            nchw = inp.permute(0, 3, 1, 2)
+            if keep_view:
+                assert nchw.is_contiguous(memory_format=ch.channels_last)
+                return nchw
+            out = dst[:nchw.shape[0]]
+            out[:] = nchw.contiguous()
+            return out
         return to_torch_image
 
     def declare_state_and_memory(self, previous_state: State) -> Tuple[State, Optional[AllocationQuery]]:
-        alloc = None
         H, W, C = previous_state.shape
-        new_type = previous_state.dtype
-        if new_type is ch.int16 and self.convert_int16:
-            new_type = ch.float16
+        dtype = previous_state.dtype
+        if dtype is ch.int16 and self.convert_int16:
+            dtype = ch.float16
             self.enable_int16conv = True
-        if not self.channels_last:
-            alloc = AllocationQuery((C, H, W), dtype=new_type, device=previous_state.device)
-        return replace(previous_state, shape=(C, H, W), dtype=new_type), alloc
+        buffer = None if self.channels_last else AllocationQuery((C, H, W), dtype=dtype,
+                                                                 device=previous_state.device)
+        return replace(previous_state, shape=(C, H, W), dtype=dtype), buffer
 
 
 class Convert(Operation):
-    """Convert to target data type (ops.py:114-136)."""
+    """Cast to ``target_dtype`` (torch ``Tensor.type``)."""
     device_aware = True
     per_sample = True
 
@@ -143,8 +144,10 @@ class Convert(Operation):
         self.target_dtype = target_dtype
 
     def generate_code(self) -> Callable:
+        target = self.target_dtype
+
         def convert(inp, dst):
-            return inp.type(self.target_dtype)
+            return inp.type(target)
         convert.is_parallel = True
         return convert
 
@@ -153,7 +156,7 @@ class Convert(Operation):
 
 
 class View(Operation):
-    """View array using np.view or torch.view (ops.py:139-160)."""
+    """Reinterpret the batch's bytes as ``target_dtype`` (``.view``)."""
     device_aware = True
     per_sample = True
 
@@ -162,10 +165,12 @@ class View(Operation):
         self.target_dtype = target_dtype
 
     def generate_code(self) -> Callable:
-        def convert(inp, dst):
-            return inp.view(self.target_dtype)
-        convert.is_parallel = True
-        return convert
+        target = self.target_dtype
+
+        def view(inp, dst):
+            return inp.view(target)
+        view.is_parallel = True
+        return view
 
     def declare_state_and_memory(self, previous_state: State) -> Tuple[State, Optional[AllocationQuery]]:
         return replace(previous_state, dtype=self.target_dtype, jit_mode=False), None

@@ -297,7 +297,8 @@ def main():
             'status': torch.full((cap,), -1, dtype=torch.int32, device=dev),
             'rstat': torch.empty(cap, dtype=torch.int32, device=dev),
             'out': torch.empty((cap, out, out, 3), dtype=out_dtype, device=dev),
-            'dec': (L.JpegDecoder(cap, int(hs.max()), int(ws.max()), int(sizes.max()))
+            'dec': (L.JpegDecoder(cap, int(hs.max()), int(ws.max()), int(sizes.max()),
+                                  L.arena_for(hs, ws, sizes, cap))
                     if mode == 'jpg' else None),
             'used': 0,
         })

@@ -104,11 +104,11 @@ struct ImgInfo {
   int32_t he[3], ve[3];  // expansion factors hmax/h, vmax/v
   int32_t cw[3], ch[3], stride[3];
   int32_t ri, rj, rh, rw;
+  // arena offset of each component's window plane, minus (wy0 * 8 * stride +
+  // wx0 * 8): plane sample (row, col) in absolute coordinates is at
+  // arena + poff + row * stride + col (stride = window width in samples)
   uint64_t poff[3];
-  // for the IDCT kernel: the window (in blocks) and block layout per
-  // component, and the ifast multipliers
-  int32_t wx0[3], wy0[3], wbw[3], wbh[3], bw[3];
-  uint64_t coff[3];
+  uint64_t rgb_off;  // K2 band staging (crop rows as RGB) for bands wider than LDS
 };
 
 // Huffman decode tables built from one image's DHT segments.  K1 runs JW
@@ -155,8 +155,12 @@ struct JShared {
   int restart;
   int ri, rj, rh, rw;
   int wx0[3], wx1[3], wy0[3], wy1[3];
-  uint64_t coff[3];
-  uint64_t poff[3];
+  uint64_t coff[3];  // first window block of each component in the coefficient region
+  uint64_t poff[3];  // see ImgInfo::poff
+  uint32_t nwin;     // window blocks (all components)
+  // this image's regions of the launch arena (bump-allocated after the parse)
+  uint64_t ds_off, cf_off, dc_off, rgb_off;
+  uint32_t ds_bytes, cf_bytes, dc_bytes;
   uint32_t dlen;
   int any;
   // per block-in-MCU descriptor for the write pass: block index of MCU (0,0)
@@ -699,19 +703,17 @@ FFCV_DEV void idct_ifast_block(int d[64], uint8_t *out, int stride) {
   }
 }
 
-// One block: load the zigzag coefficients at cp and zero them, de-zigzag +
+// One block: load the zigzag coefficients at cp, de-zigzag +
 // jidctfst.c DEQUANTIZE (int16 x int16 -> int) with the multipliers qm, and
 // the ifast IDCT into out (stride bytes per row).
 typedef int16_t s16x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
-FFCV_DEV void idct_block(int16_t *cp, const int16_t *qm, int qmax, uint8_t *out, int stride) {
+FFCV_DEV void idct_block(const int16_t *cp, const int16_t *qm, int qmax, uint8_t *out, int stride) {
   int16_t zz[64];
   int d[64];
 #pragma unroll
   for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
-#pragma unroll
-  for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);
   // max |coefficient| on packed halves (|-32768| reads as 32768 unsigned);
   // max|coef| * max|qmul| < 2^14 bounds every dequantised input, so the
   // 32-bit IDCT products are exact (else the exact 64-bit form runs)
@@ -744,15 +746,13 @@ struct JpegArgs {
   void *out;
   uint64_t out_stride;
   int32_t *status;
-  uint8_t *dstuff;
-  uint64_t dstuff_slot;
-  int16_t *coef;
-  uint64_t coef_slot;
-  uint8_t *planes;
-  uint64_t plane_slot;
-  int16_t *dcd;
-  uint64_t dcd_slot;
-  uint8_t *rgb;
+  // Per-launch scratch arena: K1 bump-allocates each image's regions (de-
+  // stuffed stream, window coefficients, DC differences, window planes, K2
+  // band staging) sized by that image's own geometry and crop window, so
+  // scratch follows the content instead of dataset-max x batch.
+  uint8_t *arena;
+  uint64_t arena_bytes;
+  unsigned long long *arena_top;  // zeroed on the stream before each K1
   ImgInfo *info;
   uint8_t *gtab;  // per-image JTables for images that cannot share the workgroup's
   uint64_t gtab_slot;
@@ -973,7 +973,6 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
   } else {
     S.color_rgb = 0;
   }
-  uint64_t off_blocks = 0, off_plane = 0;
   if (S.ncomp == 1) {
     S.cw[0] = (S.W * S.hs[0] + S.hmax - 1) / S.hmax;
     S.ch[0] = (S.H * S.vs[0] + S.vmax - 1) / S.vmax;
@@ -993,15 +992,7 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
       S.bh[c] = S.mcuy * S.vs[c];
     }
   }
-  for (int c = 0; c < S.ncomp; c++) {
-    S.coff[c] = off_blocks;
-    S.poff[c] = off_plane;
-    off_blocks += (uint64_t)S.bw[c] * S.bh[c];
-    off_plane += (uint64_t)S.bw[c] * S.bh[c] * 64;
-  }
   S.nblocks = S.mcux * S.mcuy * S.bpm;
-  if (off_blocks * 64 > a.coef_slot || off_plane > a.plane_slot || (uint64_t)S.nblocks > a.dcd_slot)
-    return FFCV_SAMPLE_TOO_LARGE;
   if (MODE == JM_COEF && (uint64_t)S.nblocks > a.max_blocks) return FFCV_SAMPLE_TOO_LARGE;
   if (MODE == JM_RRC) {
     // vector loads (the fused draws wrote the crop with vector stores in this
@@ -1039,6 +1030,12 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     S.wx0[c] = x0 >> 3;
     S.wx1[c] = x1 >> 3;
   }
+  uint32_t nwin = 0;  // coefficients / planes are stored for the window only
+  for (int c = 0; c < S.ncomp; c++) {
+    S.coff[c] = nwin;
+    nwin += (uint32_t)((S.wx1[c] - S.wx0[c] + 1) * (S.wy1[c] - S.wy0[c] + 1));
+  }
+  S.nwin = nwin;
   for (int b = 0; b < S.bpm; b++) {
     int c = S.blk_comp[b], dx = S.blk_dx[b], dy = S.blk_dy[b], hs = S.hs[c], vs = S.vs[c];
     // bx = mx * hs + dx in [wx0, wx1]  <=>  mx in [mx_lo, mx_hi]
@@ -1046,7 +1043,11 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     int mxh = S.wx1[c] - dx < 0 ? -1 : (S.wx1[c] - dx) / hs;
     int myl = S.wy0[c] - dy <= 0 ? 0 : (S.wy0[c] - dy + vs - 1) / vs;
     int myh = S.wy1[c] - dy < 0 ? -1 : (S.wy1[c] - dy) / vs;
-    S.pdesc[b][0] = make_int4((int)(S.coff[c] + (uint64_t)dy * S.bw[c] + dx), vs * S.bw[c], hs, mxl);
+    // window-relative index of block (mx * hs + dx, my * vs + dy) is
+    // base + my * (vs * wbw) + mx * hs (base may be negative: only window
+    // blocks are ever addressed, and the sum wraps back in 32 bits)
+    const int wbw = S.wx1[c] - S.wx0[c] + 1;
+    S.pdesc[b][0] = make_int4((int)S.coff[c] + (dy - S.wy0[c]) * wbw + (dx - S.wx0[c]), vs * wbw, hs, mxl);
     S.pdesc[b][1] = make_int4(mxh, myl, myh, 0);
   }
   return FFCV_SAMPLE_OK;
@@ -1220,8 +1221,8 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
     if (cur >= 0)
-      write_range(S, T, words, (uint32_t)a.dstuff_slot, g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef),
-                  (uint32_t)(a.coef_slot * 2), wave_uniform((gshort_t *)dcd), (uint32_t)(a.dcd_slot * 2), it_lane2);
+      write_range(S, T, words, S.ds_bytes, g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef), S.cf_bytes,
+                  wave_uniform((gshort_t *)dcd), S.dc_bytes, it_lane2);
   }
   if (a.dbg) {
     const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
@@ -1229,6 +1230,41 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   }
 
   return any_bad;
+}
+
+// Bump-allocate this image's regions of the launch arena (wave-uniform; lane
+// 0 does the atomic) and zero its window coefficients (the write pass stores
+// only non-zero coefficients).  Region sizes: de-stuffed stream + padding,
+// window coefficients (int16 x 64 per block), DC differences (int16 per
+// block), window planes (64 B per block), K2 band staging (crop RGB).
+FFCV_DEV uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
+FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t, int MODE) {
+  const uint64_t ds = align256((uint64_t)nbytes + 64), cf = align256((uint64_t)S.nwin * 128);
+  const uint64_t dc = align256((uint64_t)S.nblocks * 2), pl = align256((uint64_t)S.nwin * 64);
+  const uint64_t rgb = MODE == JM_RRC ? align256((uint64_t)S.rh * S.rw * 3) : 0;
+  const uint64_t need = ds + cf + dc + pl + rgb;
+  unsigned long long base = 0;
+  if (t == 0) base = atomicAdd(a.arena_top, (unsigned long long)need);
+  base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+  if (base + need > a.arena_bytes) return FFCV_SAMPLE_TOO_LARGE;  // arena exhausted
+  S.ds_off = base;
+  S.ds_bytes = (uint32_t)ds;
+  S.cf_off = base + ds;
+  S.cf_bytes = (uint32_t)cf;
+  S.dc_off = S.cf_off + cf;
+  S.dc_bytes = (uint32_t)dc;
+  const uint64_t pl_off = S.dc_off + dc;
+  S.rgb_off = pl_off + pl;
+  uint64_t o = pl_off;
+  for (int c = 0; c < S.ncomp; c++) {
+    const uint64_t wstride = (uint64_t)(S.wx1[c] - S.wx0[c] + 1) * 8;
+    S.poff[c] = o - ((uint64_t)S.wy0[c] * 8 * wstride + (uint64_t)S.wx0[c] * 8);  // wraps: see ImgInfo
+    o += wstride * (uint64_t)(S.wy1[c] - S.wy0[c] + 1) * 8;
+  }
+  uint4 *cz = (uint4 *)(a.arena + S.cf_off);
+  for (uint32_t i = (uint32_t)t; i < (uint32_t)(S.nwin * 8); i += JL) cz[i] = make_uint4(0, 0, 0, 0);
+  return FFCV_SAMPLE_OK;
 }
 
 template <int MODE>
@@ -1309,7 +1345,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   STAMP(10);
   if (t == 0) S.src = src;
   if (JL == JT || t == 0) {  // the whole wave runs the (scalar) parse; see parse_header
-    const int st = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, wave_uniform(src), nbytes, smp, a, k, MODE)) : -1;
+    int st = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, wave_uniform(src), nbytes, smp, a, k, MODE)) : -1;
+    if (st == FFCV_SAMPLE_OK) st = alloc_scratch(S, a, nbytes, t, MODE);
     if (t == 0) S.status = st;
   }
   __syncthreads();
@@ -1384,9 +1421,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     fail();
     return;
   }
-  // the coefficient slot is all zeros here: the IDCT kernel zeroes every
-  // block it consumes (and ffcv_jpeg_create zeroed the slot)
-  int16_t *coef = a.coef + a.coef_slot * k;
+  // the window coefficients were zeroed by alloc_scratch
+  int16_t *coef = (int16_t *)(a.arena + S.cf_off);
 
   // ------------------------------------------------------------- P2 ----
   // De-stuffing in stream order: each step the wave reads 64 consecutive
@@ -1394,7 +1430,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   // 0x00 after 0xFF, stops at the first marker (0xFF + non-zero), and
   // writes the kept bytes at offsets from a wave scan of their counts.
   STAMP(2);
-  uint8_t *gds = a.dstuff + a.dstuff_slot * k;
+  uint8_t *gds = a.arena + S.ds_off;
   uint32_t dlen = 0;
   {
     const uint32_t seg0 = S.scan_off;
@@ -1411,7 +1447,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     // The flush issues a fixed number of buffer stores per lane (out of range
     // past the staged bytes), so the prefetched loads issued before it are
     // waited for with a static vmcnt, not behind a dynamic store count.
-    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(gds), 0, (int)a.dstuff_slot, BUF_CFG);
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(gds), 0, (int)S.ds_bytes, BUF_CFG);
     constexpr int FL_N = (STAGE_BYTES / 4 + JL - 1) / JL;  // stores per lane per flush
     auto flush = [&](uint32_t upto) {  // write stage bytes [fbase, upto), upto % 4 == 0
       wsync_lds();
@@ -1509,7 +1545,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const uint32_t total_bits = dlen * 8;
 
 
-  int16_t *dcd = a.dcd + a.dcd_slot * k;
+  int16_t *dcd = (int16_t *)(a.arena + S.dc_off);
   const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd)
                              : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd);
   wsync_mem();
@@ -1545,7 +1581,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
       int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
       if (bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c])
-        coef[(S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64] = (int16_t)pv;
+        coef[(S.coff[c] + (uint64_t)(by - S.wy0[c]) * (S.wx1[c] - S.wx0[c] + 1) + (bx - S.wx0[c])) * 64] = (int16_t)pv;
       if (++ph == S.bpm) {
         ph = 0;
         if (++mx == S.mcux) {
@@ -1565,7 +1601,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       int my = (int)(m / S.mcux), mx = (int)(m - (int64_t)my * S.mcux);
       int c = S.blk_comp[ph];
       int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
-      const int16_t *cp = coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64;
+      const int16_t *cp = coef + (S.coff[c] + (uint64_t)by * (S.wx1[c] - S.wx0[c] + 1) + bx) * 64;  // window = image
       int16_t zz[64], nb[64];
 #pragma unroll
       for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
@@ -1574,8 +1610,6 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       uint4 *dp = (uint4 *)(o + b * 64);
 #pragma unroll
       for (int p8 = 0; p8 < 8; p8++) dp[p8] = *(const uint4 *)(nb + p8 * 8);
-#pragma unroll
-      for (int p8 = 0; p8 < 8; p8++) ((uint4 *)cp)[p8] = make_uint4(0, 0, 0, 0);  // slot back to zeros
     }
     if (t == 0) a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
     return;
@@ -1596,15 +1630,10 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       info->ve[c] = v ? S.vmax / S.vs[c] : 1;
       info->cw[c] = v ? S.cw[c] : 0;
       info->ch[c] = v ? S.ch[c] : 0;
-      info->stride[c] = v ? S.bw[c] * 8 : 0;
+      info->stride[c] = v ? (S.wx1[c] - S.wx0[c] + 1) * 8 : 0;
       info->poff[c] = v ? S.poff[c] : 0;
-      info->wx0[c] = v ? S.wx0[c] : 0;
-      info->wy0[c] = v ? S.wy0[c] : 0;
-      info->wbw[c] = v ? S.wx1[c] - S.wx0[c] + 1 : 0;
-      info->wbh[c] = v ? S.wy1[c] - S.wy0[c] + 1 : 0;
-      info->bw[c] = v ? S.bw[c] : 0;
-      info->coff[c] = v ? S.coff[c] : 0;
     }
+    info->rgb_off = S.rgb_off;
     info->ri = S.ri;
     info->rj = S.rj;
     info->rh = S.rh;
@@ -1618,7 +1647,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   // the coefficient slot all-zero for the next batch.
   STAMP(8);
   {
-    uint8_t *planes = a.planes + a.plane_slot * k;
+    uint8_t *planes = a.arena;
     int nb[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) nb[c] = c < S.ncomp ? (S.wx1[c] - S.wx0[c] + 1) * (S.wy1[c] - S.wy0[c] + 1) : 0;
@@ -1635,8 +1664,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       }
       const int wbw = S.wx1[c] - S.wx0[c] + 1;
       const int by = S.wy0[c] + j / wbw, bx = S.wx0[c] + j % wbw;
-      const int stride = S.bw[c] * 8;
-      idct_block(coef + (S.coff[c] + (uint64_t)by * S.bw[c] + bx) * 64, S.qmul[c], S.qmax[c],
+      const int stride = wbw * 8;
+      idct_block(coef + (S.coff[c] + (uint64_t)j) * 64, S.qmul[c], S.qmax[c],
                  planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
     }
   }
@@ -1791,7 +1820,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(6))) j
     }
     return;
   }
-  const uint8_t *planes = a.planes + a.plane_slot * k;
+  const uint8_t *planes = a.arena;
   const ColorGeom G = color_geom(I);
   const int ncomp = G.ncomp;
   GPlane gp[3];
@@ -2058,7 +2087,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(6))) j
   // Bands too wide for LDS stage their rows in the image's rgb slot at their
   // absolute crop-row position; rows shared with a neighbouring band are
   // written with identical bytes by both.
-  uint8_t *groi = a.rgb + a.plane_slot * k;
+  uint8_t *groi = a.arena + I.rgb_off;
   uint8_t *dst = staged ? roi : groi + (uint64_t)r0 * step;
   const bool tabs = tap_b > 0 && lut_b <= K2_LDS / 2 && !(a.k2flags & 2);
   if (tabs) {  // [0, out_w): columns, [out_w, out_w + rows): the band's rows
@@ -2240,29 +2269,19 @@ struct ffcv_jpeg_ctx {
   int max_batch;
   uint32_t max_h, max_w;
   uint64_t max_bytes;
-  uint8_t *dstuff;
-  uint64_t dstuff_slot;
-  int16_t *coef;
-  uint64_t coef_slot;
-  uint8_t *planes;
-  uint64_t plane_slot;
-  int16_t *dcd;
-  uint64_t dcd_slot;
-  uint8_t *rgb;  // K2 band staging when a band's source rows exceed LDS
+  uint8_t *arena;  // per-launch scratch, bump-allocated per image by K1
+  uint64_t arena_bytes;
+  unsigned long long *arena_top;
   ImgInfo *info;
   uint8_t *gtab;
   uint64_t gtab_slot;
-  uint64_t nblk;
 };
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 static void free_ctx(ffcv_jpeg_ctx *c) {
-  (void)hipFree(c->dstuff);
-  (void)hipFree(c->coef);
-  (void)hipFree(c->planes);
-  (void)hipFree(c->dcd);
-  (void)hipFree(c->rgb);
+  (void)hipFree(c->arena);
+  (void)hipFree(c->arena_top);
   (void)hipFree(c->info);
   (void)hipFree(c->gtab);
   delete c;
@@ -2270,8 +2289,16 @@ static void free_ctx(ffcv_jpeg_ctx *c) {
 
 extern "C" {
 
-int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, uint32_t max_width,
-                     uint64_t max_bytes) {
+uint64_t ffcv_jpeg_scratch_bound(uint32_t height, uint32_t width, uint64_t nbytes) {
+  // every region alloc_scratch can take for an image of this size, whatever
+  // its crop, sampling and MCU padding (hmax, vmax <= 4; <= 10 blocks per MCU)
+  const uint64_t blocks = 3 * ((uint64_t)(width + 7) / 8 + 4) * ((uint64_t)(height + 7) / 8 + 4);
+  return align_up(nbytes + 64, 256) + align_up(blocks * 128, 256) + align_up(blocks * 2, 256) +
+         align_up(blocks * 64, 256) + align_up((uint64_t)height * width * 3, 256);
+}
+
+int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, uint32_t max_width,
+                           uint64_t max_bytes, uint64_t arena_bytes) {
   if (!out || max_batch <= 0 || max_height == 0 || max_width == 0 || max_height > 65535 ||
       max_width > 65535 || max_bytes == 0) {
     ffcv::set_error("ffcv_jpeg_create: invalid arguments");
@@ -2283,34 +2310,26 @@ int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, ui
   c->max_h = max_height;
   c->max_w = max_width;
   c->max_bytes = max_bytes;
-  uint64_t bw = (max_width + 7) / 8 + 4, bh = (max_height + 7) / 8 + 4;
-  uint64_t nblk = 3 * bw * bh;  // all components, MCU padded (hmax, vmax <= 4)
-  c->dstuff_slot = align_up(max_bytes + 64, 256);
-  c->coef_slot = align_up(nblk * 64, 128);   // int16 elements
-  c->plane_slot = align_up(nblk * 64, 256);  // bytes
-  c->dcd_slot = align_up(nblk, 128);         // int16 elements
-  c->nblk = nblk;
+  // default: room for max_batch images of the maximum size (never exhausted)
+  c->arena_bytes = arena_bytes ? arena_bytes
+                               : (uint64_t)max_batch * ffcv_jpeg_scratch_bound(max_height, max_width, max_bytes);
   c->gtab_slot = align_up(sizeof(JTables), 256);
   hipError_t e;
-  if ((e = hipMalloc(&c->dstuff, c->dstuff_slot * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->coef, c->coef_slot * 2 * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->planes, c->plane_slot * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->dcd, c->dcd_slot * 2 * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->rgb, c->plane_slot * max_batch)) != hipSuccess ||
+  if ((e = hipMalloc(&c->arena, c->arena_bytes)) != hipSuccess ||
+      (e = hipMalloc(&c->arena_top, sizeof(unsigned long long))) != hipSuccess ||
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess ||
-      // the entropy kernel writes only non-zero coefficients into an
-      // all-zero slot; the IDCT kernel restores the zeros it consumed
-      (e = hipMemset(c->coef, 0, c->coef_slot * 2 * max_batch)) != hipSuccess ||
-      // the memset runs on the null stream, which does not order non-blocking
-      // streams (torch's): finish it before any launch can use the context
-      (e = hipDeviceSynchronize()) != hipSuccess) {
+      (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess) {
     int rc = ffcv::check_hip(e, "ffcv_jpeg_create: hipMalloc");
     free_ctx(c);
     return rc;
   }
   *out = c;
   return FFCV_OK;
+}
+
+int ffcv_jpeg_create(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_height, uint32_t max_width,
+                     uint64_t max_bytes) {
+  return ffcv_jpeg_create_arena(out, max_batch, max_height, max_width, max_bytes, 0);
 }
 
 // Diagnostic hook (not in the public header): per-image phase stamps
@@ -2344,15 +2363,9 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.base = base;
   a.samples = samples;
   a.status = status;
-  a.dstuff = c->dstuff;
-  a.dstuff_slot = c->dstuff_slot;
-  a.coef = c->coef;
-  a.coef_slot = c->coef_slot;
-  a.planes = c->planes;
-  a.plane_slot = c->plane_slot;
-  a.dcd = c->dcd;
-  a.dcd_slot = c->dcd_slot;
-  a.rgb = c->rgb;
+  a.arena = c->arena;
+  a.arena_bytes = c->arena_bytes;
+  a.arena_top = c->arena_top;
   a.info = c->info;
   a.gtab = c->gtab;
   a.gtab_slot = c->gtab_slot;
@@ -2386,6 +2399,7 @@ static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void
   a.out_stride = p->out_stride ? p->out_stride : dense;
   const int only = a.diag_only;
   if (only & 1) {
+    FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
@@ -2460,6 +2474,7 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   a.out = out;
   a.out_stride = out_stride;
   hipStream_t s = ffcv::as_stream(stream);
+  FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), s));
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
   dim3 g2((c->max_h + BAND - 1) / BAND, batch);
@@ -2478,6 +2493,7 @@ int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *
   a.out = coefs;
   a.out_stride = max_blocks * 64 * 2;
   a.max_blocks = max_blocks;
+  FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), ffcv::as_stream(stream)));
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0,
                      ffcv::as_stream(stream), a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<COEF>");

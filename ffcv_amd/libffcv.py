@@ -87,6 +87,8 @@ _SIGS = {
     'ffcv_gather_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_uint64]),
     'ffcv_jpeg_create': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64]),
     'ffcv_jpeg_destroy': (c_int, [c_void_p]),
+    'ffcv_jpeg_create_arena': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64, c_uint64]),
+    'ffcv_jpeg_scratch_bound': (c_uint64, [c_uint32, c_uint32, c_uint64]),
     'ffcv_jpeg_set_diag': (c_int, [c_void_p, c_int, c_int]),
     'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -289,17 +291,44 @@ def flip_batch(inp, out, flips, stream=None):
            'ffcv_flip_batch')
 
 
-class JpegDecoder:
-    """Owns an ffcv_jpeg_ctx (scratch for max_batch images)."""
+def scratch_bound(heights, widths, nbytes):
+    """ffcv_jpeg_scratch_bound over arrays (numpy restatement of the C
+    formula, checked against it in tests/test_abi.py): the most arena bytes
+    one image can take, whatever its crop."""
+    h = np.asarray(heights, dtype=np.uint64)
+    w = np.asarray(widths, dtype=np.uint64)
+    n = np.asarray(nbytes, dtype=np.uint64)
 
-    def __init__(self, max_batch, max_height, max_width, max_bytes):
+    def a256(x):
+        return (x + np.uint64(255)) // np.uint64(256) * np.uint64(256)
+    blocks = np.uint64(3) * ((w + np.uint64(7)) // np.uint64(8) + np.uint64(4)) * \
+        ((h + np.uint64(7)) // np.uint64(8) + np.uint64(4))
+    return (a256(n + np.uint64(64)) + a256(blocks * np.uint64(128)) + a256(blocks * np.uint64(2)) +
+            a256(blocks * np.uint64(64)) + a256(h * w * np.uint64(3)))
+
+
+def arena_for(heights, widths, nbytes, max_batch):
+    """Arena bytes that no launch of max_batch images of this dataset can
+    exhaust: the sum of the max_batch largest per-image bounds."""
+    b = scratch_bound(heights, widths, nbytes)
+    if b.size > max_batch:
+        b = np.partition(b, b.size - max_batch)[b.size - max_batch:]
+    return int(b.sum()) + 4096
+
+
+class JpegDecoder:
+    """Owns an ffcv_jpeg_ctx: launch scratch for up to max_batch images in
+    one arena of arena_bytes (default: max_batch images of the maximum size)."""
+
+    def __init__(self, max_batch, max_height, max_width, max_bytes, arena_bytes=0):
         self.handle = c_void_p()
         self.max_batch = int(max_batch)
         self.max_height, self.max_width = int(max_height), int(max_width)
         self.max_bytes = int(max_bytes)
-        _check(lib().ffcv_jpeg_create(ctypes.byref(self.handle), self.max_batch,
-                                      self.max_height, self.max_width, self.max_bytes),
-               'ffcv_jpeg_create')
+        self.arena_bytes = int(arena_bytes)
+        _check(lib().ffcv_jpeg_create_arena(ctypes.byref(self.handle), self.max_batch,
+                                            self.max_height, self.max_width, self.max_bytes,
+                                            self.arena_bytes), 'ffcv_jpeg_create')
 
     def rrc(self, base, samples, batch, crops, cutout_yx, flips, params: RRCParams, out,
             status, stream=None):

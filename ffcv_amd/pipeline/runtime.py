@@ -71,6 +71,21 @@ class DeviceDataset:
                                   int(sizes[jpg].max()) if jpg.any() else 1)
         return self._tables[f_ix]
 
+    def arena_bytes(self, f_ix, max_batch):
+        """JPEG scratch arena for launches of max_batch samples of field
+        f_ix: the sum of the largest max_batch per-image bounds (one huge image
+        in a dataset costs its own size once, not x batch)."""
+        key = (f_ix, int(max_batch))
+        if not hasattr(self, '_arena'):
+            self._arena = {}
+        if key not in self._arena:
+            from .. import libffcv as L
+            t = self.host_table(f_ix)
+            jpg = t['mode'] == 0
+            self._arena[key] = L.arena_for(t['height'][jpg], t['width'][jpg], t['size'][jpg], max_batch) \
+                if jpg.any() else 4096
+        return self._arena[key]
+
     def has_mode(self, f_ix, mode):
         self.table(f_ix)
         return self._modes[f_ix][1 if mode == 1 else 0]
@@ -211,7 +226,8 @@ class BatchContext:
         if f_ix not in self._decoders:
             from .. import libffcv as L
             h, w, nbytes = self.dataset.limits(f_ix)
-            self._decoders[f_ix] = L.JpegDecoder(self.batch_size, h, w, nbytes)
+            self._decoders[f_ix] = L.JpegDecoder(self.batch_size, h, w, nbytes,
+                                                 self.dataset.arena_bytes(f_ix, self.batch_size))
         return self._decoders[f_ix]
 
     def check_status(self, status, what):

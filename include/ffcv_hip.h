@@ -47,7 +47,7 @@ enum {
   FFCV_SAMPLE_OK = 0,
   FFCV_SAMPLE_BAD_MARKER = 1,      /* not a JPEG / truncated header */
   FFCV_SAMPLE_UNSUPPORTED = 2,     /* progressive, arithmetic, 12-bit, DRI, CMYK */
-  FFCV_SAMPLE_TOO_LARGE = 3,       /* exceeds the ctx's max_height/max_width */
+  FFCV_SAMPLE_TOO_LARGE = 3,       /* exceeds the ctx's max size or scratch arena */
   FFCV_SAMPLE_CORRUPT = 4,         /* entropy stream inconsistent */
   FFCV_SAMPLE_GEOMETRY = 5,        /* SOF size != .beton metadata */
   FFCV_SAMPLE_RNG = 6              /* > 623 MT19937 draws for one stream */
@@ -197,6 +197,20 @@ int ffcv_gather_raw_batch(void *stream, const uint8_t *base,
 typedef struct ffcv_jpeg_ctx ffcv_jpeg_ctx;
 int ffcv_jpeg_create(ffcv_jpeg_ctx **ctx, int max_batch, uint32_t max_height,
                      uint32_t max_width, uint64_t max_bytes);
+/* Scratch is one arena per context, bump-allocated per image by the entropy
+ * kernel from the image's own size and crop window (not dataset-max x
+ * batch).  ffcv_jpeg_create sizes it for max_batch images of the maximum
+ * size; ffcv_jpeg_create_arena takes the size from the caller, e.g. the sum
+ * of ffcv_jpeg_scratch_bound over the largest max_batch images of a dataset
+ * (a launch can then never exhaust it).  An image that does not fit in what
+ * is left of the arena gets FFCV_SAMPLE_TOO_LARGE. */
+int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **ctx, int max_batch,
+                           uint32_t max_height, uint32_t max_width,
+                           uint64_t max_bytes, uint64_t arena_bytes);
+/* Upper bound of the arena bytes one image of this size (and compressed
+ * size) can take, for any crop (host function, no device access). */
+uint64_t ffcv_jpeg_scratch_bound(uint32_t height, uint32_t width,
+                                 uint64_t nbytes);
 int ffcv_jpeg_destroy(ffcv_jpeg_ctx *ctx);
 
 /* rgb_image.py:185-210 jpg branch fused end to end: decode only the MCUs the

@@ -110,3 +110,18 @@ def test_host_read_and_imdecode_arguments(tmp_path, hip_lib):
     assert L.imdecode(data, out, 8, 8, enable_crop=True) == -1
     assert b'not supported' in hip_lib.ffcv_last_error()
     assert L.imdecode(data, out, 8, 8, 0, 8) == -1
+
+
+def test_scratch_bound_matches_c(hip_lib):
+    """libffcv.scratch_bound (numpy, used to size launch arenas) equals
+    ffcv_jpeg_scratch_bound; arena_for sums the largest per-image bounds."""
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(2)
+    hs = rng.integers(1, 5000, 200)
+    ws = rng.integers(1, 5000, 200)
+    ns = rng.integers(1, 3_000_000, 200)
+    got = L.scratch_bound(hs, ws, ns)
+    for h, w, n, g in zip(hs, ws, ns, got):
+        assert int(g) == L.lib().ffcv_jpeg_scratch_bound(int(h), int(w), int(n))
+    assert L.arena_for(hs, ws, ns, 10) == int(np.sort(got)[-10:].sum()) + 4096
+    assert L.arena_for(hs[:5], ws[:5], ns[:5], 10) == int(got[:5].sum()) + 4096

@@ -467,3 +467,44 @@ def test_host_imdecode_matches_libjpeg(hip_lib, oracle):
     bad[:2] = 0  # no SOI
     assert L.imdecode(bad, out, h, w, h, w) == -1
     assert L.imdecode(blobs[0], np.zeros((h + 1, w, 3), np.uint8), h + 1, w, h + 1, w) == -1
+
+
+def test_jpeg_arena_sizing_and_exhaustion(hip_lib, oracle):
+    """Scratch follows the content: a batch with one 2400x1800 image among
+    small ones decodes bit-exactly from an arena sized by arena_for (the
+    largest bounds, not batch x max); an arena too small for the batch marks
+    the images that do not fit FFCV_SAMPLE_TOO_LARGE (zero output) and decodes
+    the rest exactly."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(41)
+    imgs = [natural_image(rng, int(rng.integers(40, 120)), int(rng.integers(40, 120))) for _ in range(30)]
+    imgs.insert(7, natural_image(rng, 1800, 2400))
+    blobs = [encode_jpeg(im, 90, '4:2:0') for im in imgs]
+    hs = np.array([i.shape[0] for i in imgs])
+    ws = np.array([i.shape[1] for i in imgs])
+    ns = np.array([len(b) for b in blobs])
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    arena = L.arena_for(hs, ws, ns, B)
+    assert arena < B * int(L.scratch_bound(1800, 2400, ns.max())) // 4
+    stride = 1800 * 2400 * 3
+    for arena_bytes, expect_all in ((arena, True), (int(L.scratch_bound(120, 120, ns[:7].max())) * 5, False)):
+        dec = L.JpegDecoder(B, 1800, 2400, int(ns.max()), arena_bytes)
+        out = torch.zeros(B * stride, dtype=torch.uint8, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        dec.decode(d_buf, d_smp, B, out, stride, status)
+        torch.cuda.synchronize()
+        st = status.cpu().numpy()
+        o = out.cpu().numpy()
+        if expect_all:
+            assert (st == 0).all(), st
+        else:
+            assert (st == 0).sum() >= 1 and (st == 3).sum() >= 1 and set(st.tolist()) <= {0, 3}, st
+        for k in range(B):
+            got = o[k * stride:k * stride + hs[k] * ws[k] * 3].reshape(hs[k], ws[k], 3)
+            if st[k] == 0:
+                assert np.array_equal(got, oracle.jpeg_decode(blobs[k])), k
+            else:
+                assert not got.any()
+        dec.close()

@@ -1221,8 +1221,8 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
     if (cur >= 0)
-      write_range(S, T, words, S.ds_bytes, g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef), S.cf_bytes,
-                  wave_uniform((gshort_t *)dcd), S.dc_bytes, it_lane2);
+      write_range(S, T, words, wuni(S.ds_bytes), g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef),
+                  wuni(S.cf_bytes), wave_uniform((gshort_t *)dcd), wuni(S.dc_bytes), it_lane2);
   }
   if (a.dbg) {
     const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
@@ -1422,7 +1422,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     return;
   }
   // the window coefficients were zeroed by alloc_scratch
-  int16_t *coef = (int16_t *)(a.arena + S.cf_off);
+  // arena offsets are wave-uniform: keep them in scalar registers
+  const uint64_t cf_off = ((uint64_t)wuni((uint32_t)(S.cf_off >> 32)) << 32) | wuni((uint32_t)S.cf_off);
+  int16_t *coef = (int16_t *)(a.arena + cf_off);
 
   // ------------------------------------------------------------- P2 ----
   // De-stuffing in stream order: each step the wave reads 64 consecutive
@@ -1430,7 +1432,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   // 0x00 after 0xFF, stops at the first marker (0xFF + non-zero), and
   // writes the kept bytes at offsets from a wave scan of their counts.
   STAMP(2);
-  uint8_t *gds = a.arena + S.ds_off;
+  uint8_t *gds = a.arena + (((uint64_t)wuni((uint32_t)(S.ds_off >> 32)) << 32) | wuni((uint32_t)S.ds_off));
   uint32_t dlen = 0;
   {
     const uint32_t seg0 = S.scan_off;
@@ -1447,7 +1449,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     // The flush issues a fixed number of buffer stores per lane (out of range
     // past the staged bytes), so the prefetched loads issued before it are
     // waited for with a static vmcnt, not behind a dynamic store count.
-    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(gds), 0, (int)S.ds_bytes, BUF_CFG);
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(wave_uniform(gds), 0, (int)wuni(S.ds_bytes), BUF_CFG);
     constexpr int FL_N = (STAGE_BYTES / 4 + JL - 1) / JL;  // stores per lane per flush
     auto flush = [&](uint32_t upto) {  // write stage bytes [fbase, upto), upto % 4 == 0
       wsync_lds();
@@ -1545,7 +1547,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const uint32_t total_bits = dlen * 8;
 
 
-  int16_t *dcd = (int16_t *)(a.arena + S.dc_off);
+  int16_t *dcd = (int16_t *)(a.arena + (((uint64_t)wuni((uint32_t)(S.dc_off >> 32)) << 32) | wuni((uint32_t)S.dc_off)));
   const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd)
                              : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd);
   wsync_mem();

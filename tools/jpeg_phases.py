@@ -8,6 +8,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from ffcv_amd import libffcv as L
+if len(sys.argv) > 2:
+    L.LIB_PATH = os.path.abspath(sys.argv[2])  # a -DFFCV_K1_DIAG build (tools/build_variant.sh)
 from bench import make_unique, IMAGENET_MEAN, IMAGENET_STD
 from ffcv_amd.transforms.lut import make_lut
 

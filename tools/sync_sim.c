@@ -275,6 +275,70 @@ int main(int argc, char **argv) {
     printf("symbols %ld steps %ld (%.3f steps/symbol) PB %d MS %d DCP %d\n", nsym, nstep, (double)nstep / nsym, PB, MS, DCP);
     return 0;
   }
+  if (heur == 10) {  // phase-probe heuristic: pick the start phase with the fewest implausible
+                     // symbols over the first M symbols, then measure its phase-sync distance
+    int M = getenv("SIM_PROBE") ? atoi(getenv("SIM_PROBE")) : 40;
+    int8_t *tph = malloc(tbits + 64);
+    memset(tph, -1, tbits + 64);
+    uint32_t pos = 0;
+    int z = 0, ph = 0;
+    while (pos < tbits) {
+      if (z == 0) tph[pos] = ph;
+      int len, bad, ti = z == 0 ? ph_dc[ph] : ph_ac[ph];
+      int v = sym(ti, pos, &len, &bad);
+      int sz = z == 0 ? v : (v & 15), r = z == 0 ? 0 : v >> 4;
+      pos += len + sz;
+      int zac = sz ? z + r + 1 : (r == 15 ? z + 16 : 64);
+      z = z == 0 ? 1 : zac;
+      if (z >= 64) { z = 0; ph = (ph + 1) % bpm; }
+    }
+    srand(1);
+    long s0sum = 0, sbsum = 0, s0max = 0, sbmax = 0, n = 0, right = 0;
+    for (int smp = 0; smp < 400; smp++) {
+      uint32_t s0 = (uint32_t)(((double)rand() / RAND_MAX) * (tbits * 0.8));
+      int bestg = 0; long bestscore = 1L << 40;
+      for (int g = 0; g < bpm; g++) {
+        uint32_t q = s0; int zz = 0, pp = g; long score = 0;
+        for (int k = 0; k < M && q < tbits; k++) {
+          int len, bad, ti = zz == 0 ? ph_dc[pp] : ph_ac[pp];
+          int v = sym(ti, q, &len, &bad);
+          int sz = zz == 0 ? v : (v & 15), r = zz == 0 ? 0 : v >> 4;
+          int inval = bad || (zz == 0 ? sz > 11 : (sz > 10 || (sz && zz + r > 63)));
+          score += inval ? 100 : 0;
+          score += zz == 0 ? 0 : 0;
+          q += len + sz;
+          int zac = sz ? zz + r + 1 : (r == 15 ? zz + 16 : 64);
+          if (zz && zac > 64) score += 100;
+          zz = zz == 0 ? 1 : zac;
+          if (zz >= 64) { zz = 0; pp = (pp + 1) % bpm; }
+        }
+        if (score < bestscore) { bestscore = score; bestg = g; }
+      }
+      long dist[2];
+      for (int w = 0; w < 2; w++) {
+        int g = w ? bestg : 0;
+        uint32_t q = s0; int zz = 0, pp = g; long k = 0, ps = -1;
+        while (q < tbits && k < 200000) {
+          if (zz == 0 && tph[q] == pp) { ps = k; break; }
+          int len, bad, ti = zz == 0 ? ph_dc[pp] : ph_ac[pp];
+          int v = sym(ti, q, &len, &bad);
+          int sz = zz == 0 ? v : (v & 15), r = zz == 0 ? 0 : v >> 4;
+          q += len + sz; k++;
+          int zac = sz ? zz + r + 1 : (r == 15 ? zz + 16 : 64);
+          zz = zz == 0 ? 1 : zac;
+          if (zz >= 64) { zz = 0; pp = (pp + 1) % bpm; }
+        }
+        dist[w] = ps < 0 ? k : ps;
+      }
+      s0sum += dist[0]; sbsum += dist[1]; n++;
+      if (dist[0] > s0max) s0max = dist[0];
+      if (dist[1] > sbmax) sbmax = dist[1];
+      right += dist[1] < 40;
+    }
+    printf("probe M=%d: guess0 mean %.1f max %ld | probe mean %.1f max %ld | synced<40 %.2f\n", M,
+           (double)s0sum / n, s0max, (double)sbsum / n, sbmax, (double)right / n);
+    return 0;
+  }
   if (heur == 9) {  // sync-distance statistics from random starts
     int8_t *tph = malloc(tbits + 64);
     memset(tph, -1, tbits + 64);

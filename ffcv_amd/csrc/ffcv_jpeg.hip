@@ -1307,8 +1307,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     a.status[k] = FFCV_SAMPLE_OK;
     info->status = -1;  // K2 skips
   }
-  const uint8_t *src = a.base + smp.offset;
-  const uint32_t nbytes = (uint32_t)smp.size;
+  const uint8_t *src = wave_uniform(a.base + smp.offset);
+  const uint32_t nbytes = wuni((uint32_t)smp.size);  // uniform: sizes buffer resources
   auto fail = [&]() {
     if (t == 0) {
       a.status[k] = S.status;
@@ -1435,7 +1435,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   uint8_t *gds = a.arena + (((uint64_t)wuni((uint32_t)(S.ds_off >> 32)) << 32) | wuni((uint32_t)S.ds_off));
   uint32_t dlen = 0;
   {
-    const uint32_t seg0 = S.scan_off;
+    const uint32_t seg0 = wuni(S.scan_off);  // uniform: sizes the buffer resource below
     const uint32_t seglen = nbytes > seg0 ? nbytes - seg0 : 0;
     const uintptr_t sb = (uintptr_t)(src + seg0);
     const uint32_t mis = (uint32_t)(sb & 3);

@@ -1800,7 +1800,10 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
 };
 
 template <int MODE, bool FP16>
-__global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(6))) jpeg_color_resize_kernel(JpegArgs a) {  // 6 WGs per CU (K2_LDS)
+#ifndef K2_WPE
+#define K2_WPE 6  // waves per SIMD K2 is compiled for (6 WGs per CU at K2_LDS)
+#endif
+__global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE))) jpeg_color_resize_kernel(JpegArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint16_t *s_lut = (uint16_t *)lds;  // 768 entries (FP16)
   const int t = threadIdx.x;

@@ -208,6 +208,9 @@ def main():
     ap.add_argument('--k2flags', type=int, default=0, help='diagnostic: K2 timing-only flags')
     ap.add_argument('--only', type=int, default=0,
                     help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 2 K2)')
+    ap.add_argument('--entropy-index', action='store_true',
+                    help='later-epoch rate: attach an entropy index, fill it with one untimed pass over '
+                         'the timed samples (epoch 0), then time epoch 1 (new crops, no sync rounds)')
     args = ap.parse_args()
 
     import torch
@@ -320,6 +323,11 @@ def main():
     dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
     dp.loader_seed = 0
     dp.epoch = 0
+    eidx = None
+    if args.entropy_index and mode == 'jpg':
+        eidx = torch.zeros((N, L.EIDX_LANES, L.EIDX_WORDS), dtype=torch.int32, device=dev)
+        for sl in slots:
+            sl['dec'].set_entropy_index(eidx)
     torch.cuda.synchronize()
 
     launch_no = [0]
@@ -384,6 +392,12 @@ def main():
     run_batches(prime_batches, args.warmup)
     torch.cuda.synchronize()
     check_status('warmup')
+    if eidx is not None:
+        # the previous epoch: decodes (and indexes) exactly the timed samples
+        run_batches(prime_batches + args.warmup, args.steps)
+        torch.cuda.synchronize()
+        check_status('the indexing pass')
+        dp.epoch = 1
     for sl in slots:
         sl['status'].fill_(-1)
         sl['used'] = 0
@@ -486,6 +500,7 @@ def main():
                    'per_gpu_batch': batch, 'batches_per_launch': G, 'launches_in_flight': S,
                    'timed_launches': len(events), 'dataset_size': N,
                    'mean_sample_bytes': round(mean_bytes, 1),
+                   'entropy_index': eidx is not None,
                    'hip_hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'HIP default (4)'),
                    'parallelism': f'dp{world} (traversal-order sharding, no collectives)'},
         'roofline': roof,

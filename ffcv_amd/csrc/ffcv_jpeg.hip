@@ -774,6 +774,13 @@ struct JpegArgs {
                 // bit 7 the linear fast path; timing only: bits 8 / 9 / 10 skip the fast
                 // path's colour pass / column walk / tile staging
   int diag_only;  // host side only: kernels the launch runs (ffcv_jpeg_set_diag)
+  // Entropy index (ffcv_jpeg_set_entropy_index): per dataset sample, the
+  // converged start state of every lane range of the sync pass.  A sample
+  // decoded once with the index attached records it; later decodes of the
+  // same sample (later epochs) skip the sync rounds.  Fused launches only
+  // (the sample id comes from ids[k]).
+  uint32_t *eidx;
+  uint64_t eidx_n;
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1153,16 +1160,51 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
 
 // P3-P5 with table set T (the workgroup's LDS copy or the image's global
 // copy; separate instantiations so each reads its own address space).
+// Entropy index record of one sample: EIDX_WORDS words per lane range,
+// [pos, z | ph << 8, first block], and lane 0's second word carries
+// EIDX_VALID | nthr << 16 once the whole record is published.
+#define EIDX_LANES 64
+#define EIDX_WORDS 3
+#define EIDX_VALID 0x80000000u
 template <class TB>
 FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, int sg, const uint32_t *words,
-                             uint32_t total_bits, int16_t *coef, int16_t *dcd) {
-  // ------------------------------------------------------------- P3 ----
-  STAMP(3);
+                             uint32_t total_bits, int16_t *coef, int16_t *dcd, uint64_t sample_id) {
   uint32_t nthr = (total_bits + 191) / 192;
   nthr = max(1u, min(nthr, (uint32_t)JL));
   const uint32_t cbits = (total_bits + nthr - 1) / nthr;
   const bool active = t < (int)nthr;
   const uint32_t my_end = active ? (t == (int)nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
+  // ---------------------------------------------------- entropy index ----
+  uint32_t *rec = nullptr;
+  if (a.eidx && JL == EIDX_LANES && sample_id < a.eidx_n) rec = a.eidx + sample_id * (EIDX_LANES * EIDX_WORDS);
+  if (rec) {
+    uint32_t head = 0;
+    if (t == 0) head = __hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    head = __builtin_amdgcn_readfirstlane(head);
+    if ((head & EIDX_VALID) && ((head >> 16) & 0xff) == nthr) {
+      // published by an earlier decode of this sample: acquire, then every
+      // lane starts from its exact state (no sync rounds, no block scan)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      STAMP(3);
+      STAMP(4);
+      STAMP(5);
+      if (active) {
+        DecState g;
+        g.pos = __builtin_nontemporal_load(rec + EIDX_WORDS * t);
+        const uint32_t zp = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 1) & 0xffffu;
+        g.z = (int)(zp & 0xff);
+        g.ph = (int)(zp >> 8);
+        const uint32_t cur = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 2);
+        uint32_t it_lane2 = 0;
+        if (g.pos < my_end)
+          write_range(S, T, words, wuni(S.ds_bytes), g, my_end, cur, wave_uniform((gshort_t *)coef),
+                      wuni(S.cf_bytes), wave_uniform((gshort_t *)dcd), wuni(S.dc_bytes), it_lane2);
+      }
+      return false;
+    }
+  }
+  // ------------------------------------------------------------- P3 ----
+  STAMP(3);
   DecState g;
   g.pos = active ? t * cbits : 0;
   g.z = 0;
@@ -1214,6 +1256,18 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
     bad_lane = cur < 0 || (cur % S.bpm) != g.ph;  // inconsistent stream
   }
   const bool any_bad = seg_any(bad_lane, sg);
+  if (rec && !any_bad) {  // publish this sample's converged lane states
+    if (active) {
+      const int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
+      rec[EIDX_WORDS * t] = g.pos;
+      if (t > 0) rec[EIDX_WORDS * t + 1] = (uint32_t)g.z | ((uint32_t)g.ph << 8);
+      rec[EIDX_WORDS * t + 2] = (uint32_t)cur;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the record before its header
+    if (t == 0)
+      __hip_atomic_store(rec + 1, (uint32_t)g.z | ((uint32_t)g.ph << 8) | (nthr << 16) | EIDX_VALID, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   // ------------------------------------------------------------- P5 ----
   STAMP(5);
@@ -1548,8 +1602,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 
 
   int16_t *dcd = (int16_t *)(a.arena + (((uint64_t)wuni((uint32_t)(S.dc_off >> 32)) << 32) | wuni((uint32_t)S.dc_off)));
-  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd)
-                             : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd);
+  const uint64_t sid = a.ids && a.eidx ? a.ids[k] : ~0ull;
+  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid)
+                             : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid);
   wsync_mem();
 
   // ------------------------------------------------------------- P6 ----
@@ -2280,6 +2335,8 @@ struct ffcv_jpeg_ctx {
   ImgInfo *info;
   uint8_t *gtab;
   uint64_t gtab_slot;
+  uint32_t *eidx;  // entropy index (caller-owned), or NULL
+  uint64_t eidx_n;
 };
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -2356,6 +2413,16 @@ int ffcv_jpeg_set_diag(ffcv_jpeg_ctx *c, int only, int k2flags) {
   return FFCV_OK;
 }
 
+int ffcv_jpeg_set_entropy_index(ffcv_jpeg_ctx *c, uint32_t *index, uint64_t n_samples) {
+  if (!c || (!index && n_samples)) {
+    ffcv::set_error("ffcv_jpeg_set_entropy_index: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  c->eidx = index;
+  c->eidx_n = index ? n_samples : 0;
+  return FFCV_OK;
+}
+
 int ffcv_jpeg_destroy(ffcv_jpeg_ctx *c) {
   if (c) free_ctx(c);
   return FFCV_OK;
@@ -2372,6 +2439,8 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.arena_bytes = c->arena_bytes;
   a.arena_top = c->arena_top;
   a.info = c->info;
+  a.eidx = c->eidx;
+  a.eidx_n = c->eidx_n;
   a.gtab = c->gtab;
   a.gtab_slot = c->gtab_slot;
   a.max_h = c->max_h;

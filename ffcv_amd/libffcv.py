@@ -90,6 +90,7 @@ _SIGS = {
     'ffcv_jpeg_create_arena': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64, c_uint64]),
     'ffcv_jpeg_scratch_bound': (c_uint64, [c_uint32, c_uint32, c_uint64]),
     'ffcv_jpeg_set_diag': (c_int, [c_void_p, c_int, c_int]),
+    'ffcv_jpeg_set_entropy_index': (c_int, [c_void_p, c_void_p, c_uint64]),
     'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'ffcv_jpeg_rrc_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
@@ -316,6 +317,9 @@ def arena_for(heights, widths, nbytes, max_batch):
     return int(b.sum()) + 4096
 
 
+EIDX_LANES, EIDX_WORDS = 64, 3  # entropy index record: words per lane range
+
+
 class JpegDecoder:
     """Owns an ffcv_jpeg_ctx: launch scratch for up to max_batch images in
     one arena of arena_bytes (default: max_batch images of the maximum size)."""
@@ -355,6 +359,22 @@ class JpegDecoder:
         """Diagnostics: kernels a launch runs (bit 0 K1, bit 2 K2) and K2
         timing-only flags, fixed on this context (never read per launch)."""
         _check(lib().ffcv_jpeg_set_diag(self.handle, int(only), int(k2flags)), 'ffcv_jpeg_set_diag')
+
+    def set_entropy_index(self, index):
+        """Attach (or, with None, detach) an entropy index: a zeroed uint32
+        device tensor of shape (n_samples, 64, 3) that fused launches fill
+        and then use to skip the Huffman sync of samples decoded before."""
+        if index is None:
+            _check(lib().ffcv_jpeg_set_entropy_index(self.handle, None, 0), 'ffcv_jpeg_set_entropy_index')
+            self._eidx = None
+            return
+        if index.dim() != 3 or tuple(index.shape[1:]) != (EIDX_LANES, EIDX_WORDS) or \
+                index.element_size() != 4 or not index.is_contiguous() or not index.is_cuda:
+            raise ValueError('entropy index must be a contiguous 4-byte device tensor of shape '
+                             f'(n, {EIDX_LANES}, {EIDX_WORDS})')
+        _check(lib().ffcv_jpeg_set_entropy_index(self.handle, _p(index), int(index.shape[0])),
+               'ffcv_jpeg_set_entropy_index')
+        self._eidx = index  # keep it alive while attached
 
     def coefficients(self, base, samples, batch, out, max_blocks, status, stream=None):
         _check(lib().ffcv_jpeg_coefficients_batch(self.handle, _stream(stream), _p(base),

@@ -112,6 +112,12 @@ class Loader:
         Consecutive batches decoded by one launch sequence when every
         operation is per-sample (default: enough batches for ~6k samples,
         which fills the MI355X; 1 when the graph mixes samples).
+    entropy_index : bool (keyword only, new)
+        With ``device_cache``: keep, per JPEG field, 768 bytes of HBM per
+        sample recording where each lane range of the parallel Huffman
+        decode starts (default True).  The first decode of a sample fills
+        its record; later epochs skip the synchronisation rounds.  Output is
+        bit-identical with or without it.
     """
 
     def __init__(self, fname: str, batch_size: int, num_workers: int = -1,
@@ -121,7 +127,8 @@ class Loader:
                  pipelines: Mapping[str, Sequence[Union[Operation, ch.nn.Module]]] = {},
                  custom_fields: Mapping[str, Type[Field]] = {}, drop_last: bool = True,
                  batches_ahead: int = 3, recompile: bool = False, order_kwargs: dict = dict(),
-                 *, device=None, device_cache: bool = True, batches_per_launch: int = None):
+                 *, device=None, device_cache: bool = True, batches_per_launch: int = None,
+                 entropy_index: bool = True):
         if distributed and order == OrderOption.RANDOM and (seed is None):
             print('Warning: no ordering seed was specified with distributed=True. '
                   'Setting seed to 0 to match PyTorch distributed sampler.')
@@ -135,7 +142,7 @@ class Loader:
             'indices': indices, 'pipelines': pipelines, 'drop_last': drop_last,
             'batches_ahead': batches_ahead, 'recompile': recompile, 'device': device,
             'device_cache': device_cache, 'custom_fields': custom_fields,
-            'batches_per_launch': batches_per_launch,
+            'batches_per_launch': batches_per_launch, 'entropy_index': entropy_index,
         }
         self.batches_per_launch = batches_per_launch
         self._active_iterator = None
@@ -182,7 +189,8 @@ class Loader:
             if device_cache:
                 from ..memory_managers.device_cache import upload_file
                 data = upload_file(self.fname, self.device)
-            self.device_dataset = DeviceDataset(self.reader, self.memory_manager, self.device, data)
+            self.device_dataset = DeviceDataset(self.reader, self.memory_manager, self.device, data,
+                                                entropy_index=entropy_index and data is not None)
             if data is None:
                 self.device_dataset.staged = True
         else:

@@ -29,8 +29,10 @@ def set_current(ctx):
 class DeviceDataset:
     """Device-side view of one .beton: bytes in HBM + descriptor tables."""
 
-    def __init__(self, reader, memory_manager, device, data=None, data_base=0):
+    def __init__(self, reader, memory_manager, device, data=None, data_base=0, entropy_index=False):
         self.reader = reader
+        self.use_entropy_index = entropy_index
+        self._eidx = {}
         self.memory_manager = memory_manager
         self.device = device
         self.data = data              # torch uint8 tensor (file bytes) on device
@@ -85,6 +87,19 @@ class DeviceDataset:
             self._arena[key] = L.arena_for(t['height'][jpg], t['width'][jpg], t['size'][jpg], max_batch) \
                 if jpg.any() else 4096
         return self._arena[key]
+
+    def entropy_index(self, f_ix):
+        """Zeroed (N, 64, 3) uint32 records of field f_ix shared by every
+        slot's decoder (ffcv_jpeg_set_entropy_index), or None."""
+        if not self.use_entropy_index or self.data is None or not self.has_mode(f_ix, 0):
+            return None
+        if f_ix not in self._eidx:
+            from .. import libffcv as L
+            n = len(self.host_table(f_ix))
+            self._eidx[f_ix] = ch.zeros((n, L.EIDX_LANES, L.EIDX_WORDS), dtype=ch.int32,
+                                        device=self.device)
+            ch.cuda.synchronize(self.device)  # zeroed before any slot stream reads it
+        return self._eidx[f_ix]
 
     def has_mode(self, f_ix, mode):
         self.table(f_ix)
@@ -226,8 +241,12 @@ class BatchContext:
         if f_ix not in self._decoders:
             from .. import libffcv as L
             h, w, nbytes = self.dataset.limits(f_ix)
-            self._decoders[f_ix] = L.JpegDecoder(self.batch_size, h, w, nbytes,
-                                                 self.dataset.arena_bytes(f_ix, self.batch_size))
+            dec = L.JpegDecoder(self.batch_size, h, w, nbytes,
+                                self.dataset.arena_bytes(f_ix, self.batch_size))
+            eidx = self.dataset.entropy_index(f_ix)
+            if eidx is not None:
+                dec.set_entropy_index(eidx)
+            self._decoders[f_ix] = dec
         return self._decoders[f_ix]
 
     def check_status(self, status, what):

@@ -239,6 +239,17 @@ int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *ctx, void *stream, const uint8_t *base,
                         ffcv_sample *samples_out, const ffcv_rrc_params *p,
                         void *out, int32_t *status);
 
+/* Entropy index: index[n_samples][64][3] uint32, zero-initialised and owned
+ * by the caller (768 B per dataset sample).  With it attached, a
+ * ffcv_jpeg_rrc_fused decode of dataset sample ids[k] that finds no record
+ * runs the self-synchronising Huffman sync and publishes the converged start
+ * state of each lane range; a later decode of the same sample (the next
+ * epoch) reads it and skips the sync rounds.  Output is bit-identical either
+ * way.  NULL detaches.  Records are published with agent-scope release /
+ * acquire, so launches on other streams may read them concurrently. */
+int ffcv_jpeg_set_entropy_index(ffcv_jpeg_ctx *ctx, uint32_t *index,
+                                uint64_t n_samples);
+
 /* rgb_image.py:123-136 SimpleRGBImageDecoder jpg branch (imdecode into the
  * destination, full image) -> device [B][H][W][3] with out_stride bytes per
  * sample. */

@@ -434,6 +434,65 @@ def test_jpeg_rrc_fused_matches_staged(hip_lib, oracle):
         assert np.array_equal(res[1][4][k], want[0]), k
 
 
+def test_jpeg_entropy_index(hip_lib, oracle):
+    """ffcv_jpeg_set_entropy_index: a fused launch with the index attached
+    publishes one record per good sample (a duplicate id in the launch
+    included); a second launch that starts every lane from the records gives
+    the same bytes as a launch without the index; out-of-range ids and
+    corrupt samples publish nothing."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(41)
+    imgs, blobs = _jpeg_set(rng, 36)
+    junk = rng.integers(0, 256, 3000).astype(np.uint8)
+    blobs = blobs + [junk]
+    imgs = imgs + [imgs[0]]
+    buf, offs, sizes = pack(blobs)
+    hs = [i.shape[0] for i in imgs]
+    ws = [i.shape[1] for i in imgs]
+    n = len(imgs)
+    table = _samples(offs, sizes, hs, ws, np.zeros(n))
+    d_buf, d_table = _upload(buf), _dev(table)
+    ids = np.concatenate([rng.permutation(n), [3, 10 ** 6]]).astype(np.int64)
+    B = len(ids)
+    d_ids = torch.from_numpy(ids).to('cuda:0')
+    dp = L.DrawParams()
+    dp.out_h = dp.out_w = 160
+    dp.scale[0], dp.scale[1] = 0.08, 1.0
+    dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
+    dp.loader_seed = 5
+    rp = L.RRCParams()
+    rp.out_h = rp.out_w = 160
+    dec = L.JpegDecoder(B, max(hs), max(ws), max(len(b) for b in blobs))
+    index = torch.zeros((n, L.EIDX_LANES, L.EIDX_WORDS), dtype=torch.int32, device='cuda:0')
+
+    def run(epoch):
+        dp.epoch = epoch
+        crops = torch.empty((B, 4), dtype=torch.int32, device='cuda:0')
+        out = torch.zeros((B, 160, 160, 3), dtype=torch.uint8, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        dec.rrc_fused(d_buf, d_table, d_ids, dp, crops, None, None, rp, out, status)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), status.cpu().numpy()
+
+    plain = [run(e) for e in (0, 1)]
+    dec.set_entropy_index(index)
+    first = run(0)
+    head = index[:, 0, 1].cpu().numpy().astype(np.uint32)
+    assert (head[:n - 1] & 0x80000000).all() and head[n - 1] == 0
+    assert ((head[:n - 1] >> 16) & 0xff).max() == 64
+    rec = index.cpu().numpy().copy()
+    second = run(1)  # another epoch: other crops, every lane from its record
+    assert np.array_equal(index.cpu().numpy(), rec)
+    for (po, ps), (xo, xs) in zip(plain, (first, second)):
+        assert np.array_equal(ps, xs) and np.array_equal(po, xo)
+    assert (first[1][:B - 1] == 0).sum() == n and first[1][-1] != 0
+    dec.set_entropy_index(None)
+    assert np.array_equal(run(1)[0], plain[1][0])
+    with pytest.raises(ValueError):
+        dec.set_entropy_index(torch.zeros((n, 64, 2), dtype=torch.int32, device='cuda:0'))
+
+
 def test_host_imdecode_matches_libjpeg(hip_lib, oracle):
     """libffcv.cpp:53-112 imdecode (reference signature, host buffers in and
     out) executed by the gfx950 kernels: bit-exact with libjpeg-turbo ifast

@@ -381,3 +381,34 @@ def test_cpu_device_loader_jpeg(tmpdir_m, oracle):
         for k in range(4):
             i = int(np.nonzero([np.array_equal(oracle.jpeg_decode(s[0]), images[k].numpy()) for s in s2])[0][0])
             assert int(labels[k]) == i % 10
+
+
+def test_entropy_index_epochs_match(tmpdir_m, oracle):
+    """The entropy index (default on with device_cache) changes no output:
+    three epochs with it equal three epochs without it, every sample's record
+    is published after the first epoch, and large images use all 64 lane
+    ranges; the last epoch is also checked against the oracle."""
+    fn = os.path.join(tmpdir_m, 'eidx.beton')
+    write(fn, NaturalDS(48, hw=(300, 380), var=True, seed=21),
+          {'image': RGBImageField(write_mode='jpg', jpeg_quality=90), 'label': IntField()})
+    samples = _samples(fn)
+    lut = oracle.normalize_lut(MEAN, STD)
+    a = _c3_loader(fn, 21, entropy_index=False)
+    b = _c3_loader(fn, 21)
+    assert a.device_dataset.entropy_index(0) is None
+    for epoch in range(3):
+        order = np.random.default_rng(21 + epoch).permutation(48)
+        for bi, ((ia, la), (ib, lb)) in enumerate(zip(a, b)):
+            assert ch.equal(la, lb)
+            assert ch.equal(ia.view(ch.int16), ib.view(ch.int16))
+            if epoch == 2:
+                ids = order[bi * 16:(bi + 1) * 16]
+                want = _expected(oracle, samples, ids, 21, epoch, (64, 64), cutout=12,
+                                 fill=(124, 116, 103), lut=lut)
+                assert np.array_equal(ib.permute(0, 2, 3, 1).cpu().numpy().view(np.uint16),
+                                      want.view(np.uint16))
+        if epoch == 0:
+            head = b.device_dataset.entropy_index(0)[:, 0, 1].cpu().numpy().astype(np.uint32)
+            assert (head & 0x80000000).all()
+            nthr = (head >> 16) & 0xff
+            assert nthr.max() == 64 and nthr.min() >= 1

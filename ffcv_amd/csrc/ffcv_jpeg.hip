@@ -94,6 +94,9 @@
 #ifndef JW
 #define JW 4  // waves per K1 workgroup
 #endif
+#ifndef K1_PAD
+#define K1_PAD 0  // extra (unused) dynamic LDS per K1 workgroup: caps K1 workgroups per CU (A/B knob)
+#endif
 
 enum JMode { JM_RRC = 0, JM_FULL = 1, JM_COEF = 2 };
 
@@ -2474,7 +2477,8 @@ static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void
   const int only = a.diag_only;
   if (only & 1) {
     FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
+    hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), K1_PAD,
+                       s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);

@@ -11,7 +11,8 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
 timeout -k 10 300 python bench.py --config c5 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench_c5.log 2>&1
 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_bench_c2.log 2>&1
-for f in bench_driver bench bench_c5 bench_c2; do tail -1 gpurun_out/${TAG}_$f.log | cut -c1-200; done
+timeout -k 10 300 python bench.py --entropy-index --no-cpu-baseline > gpurun_out/${TAG}_bench_eidx.log 2>&1
+for f in bench_driver bench bench_c5 bench_c2 bench_eidx; do tail -1 gpurun_out/${TAG}_$f.log | cut -c1-200; done
 bash tools/profile.sh ${TAG}_c3 --steps 48 --warmup 12 --no-cpu-baseline
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c3 6144 gpurun_out/${TAG}_c3_summary.json > /dev/null
 bash tools/profile.sh ${TAG}_c5 --config c5 --steps 48 --warmup 12 --no-cpu-baseline

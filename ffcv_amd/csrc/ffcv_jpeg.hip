@@ -112,7 +112,27 @@ struct ImgInfo {
   // arena + poff + row * stride + col (stride = window width in samples)
   uint64_t poff[3];
   uint64_t rgb_off;  // K2 band staging (crop rows as RGB) for bands wider than LDS
+  // RRC: the crop's resize plan, and whether K1 wrote the image's linear tap
+  // table (JpegArgs::taps: out_w column taps, flip applied, then out_h row
+  // taps), computed once per image instead of once per K2 workgroup
+  ResizePlan plan;
+  int32_t taps;
 };
+
+// Linear taps (resize.cpp linear coefficients, LinTap) packed in 8 bytes:
+// x = source index | border << 31, y = c0 | c1 << 16 (0 <= c0, c1 <= 2048).
+#define K2_TAPS 512  // tap table entries per image: out_w + out_h <= 512
+FFCV_DEV uint2 tap_pack(const LinTap &l) {
+  return make_uint2((uint32_t)l.s | ((uint32_t)l.border << 31), (uint32_t)(l.c0 & 0xffff) | ((uint32_t)l.c1 << 16));
+}
+FFCV_DEV LinTap tap_unpack(uint2 v) {
+  LinTap l;
+  l.s = (int)(v.x & 0x7fffffffu);
+  l.border = (int)(v.x >> 31);
+  l.c0 = (int)(int16_t)(v.y & 0xffff);
+  l.c1 = (int)(int16_t)(v.y >> 16);
+  return l;
+}
 
 // Huffman decode tables built from one image's DHT segments.  K1 runs JW
 // images per workgroup; images whose tables (and table slots) are byte-
@@ -757,6 +777,7 @@ struct JpegArgs {
   uint64_t arena_bytes;
   unsigned long long *arena_top;  // zeroed on the stream before each K1
   ImgInfo *info;
+  uint2 *taps;    // K2_TAPS packed linear taps per image (RRC), written by K1
   uint8_t *gtab;  // per-image JTables for images that cannot share the workgroup's
   uint64_t gtab_slot;
   int batch;
@@ -1700,6 +1721,22 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     info->rw = S.rw;
     a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
   }
+  if (MODE == JM_RRC) {  // the resize plan and linear taps K2's workgroups share
+    const int out_h = a.p.out_h, out_w = a.p.out_w;
+    const ResizePlan P = make_plan(S.rw, S.rh, out_w, out_h);
+    const bool tabs = a.taps && P.kind == 3 && out_w + out_h <= K2_TAPS;
+    if (tabs) {
+      const int flip = a.flips ? a.flips[k] : 0;
+      uint2 *tp = a.taps + (uint64_t)k * K2_TAPS;
+      for (int i = t; i < out_w + out_h; i += JL)
+        tp[i] = tap_pack(i < out_w ? lin_tap(P.scale_x, P.inv_x, P.sw, flip ? out_w - 1 - i : i)
+                                   : lin_tap(P.scale_y, P.inv_y, P.sh, i - out_w));
+    }
+    if (t == 0) {
+      info->plan = P;
+      info->taps = tabs;
+    }
+  }
 
   // ------------------------------------------------------------- P8 ----
   // de-zigzag + dequantise + ifast IDCT (jidctfst.c) of the window's blocks,
@@ -1912,7 +1949,8 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       if (u * K2T + t < 768) s_lut[u * K2T + t] = lv[u];
   }
   const int ri = I.ri, rj = I.rj, rh = I.rh, rw = I.rw;
-  ResizePlan P = make_plan(rw, rh, out_w, out_h);
+  const ResizePlan P = MODE == JM_RRC ? I.plan : make_plan(rw, rh, out_w, out_h);  // RRC: K1's plan
+  const uint2 *taps = MODE == JM_RRC && I.taps ? a.taps + (uint64_t)k * K2_TAPS : nullptr;
   int r0, r1;
   band_rows(P, oy0, oy1, &r0, &r1);
   const int nrows = r1 - r0 + 1;
@@ -1936,7 +1974,13 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
   // words].  Each thread owns one output column pair and walks its half of
   // the band's rows, keeping the two source rows' horizontal sums in
   // registers (resize.cpp HResizeLinear -> VResizeLinearVec_32s8u).
-  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && !(a.k2flags & 128)) {
+  // expansion factors 1 / 2 / 4 (every common subsampling): the tile bounds
+  // below divide by shifts (a runtime x / ve compiles to a ~25-instruction
+  // VALU sequence, twelve per workgroup); 3 takes the general path
+  auto p2 = [](int x) { return x == 1 || x == 2 || x == 4; };
+  const bool pow2 = p2(G.he[0]) && p2(G.ve[0]) && p2(G.he[1]) && p2(G.ve[1]) && p2(G.he[2]) && p2(G.ve[2]);
+  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && pow2 &&
+      !(a.k2flags & 128)) {
     const int lut_b = FP16 ? 1536 : 0;
     LinTap *rtab = (LinTap *)(lds + lut_b);
     int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
@@ -1947,9 +1991,9 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
         ty0[c] = tx0[c] = trows[c] = tpitch[c] = toff[c] = 0;
         continue;
       }
-      const int he = G.he[c], ve = G.ve[c];
-      int y0 = (ri + r0) / ve - (ve == 2 ? 1 : 0), y1 = (ri + r1) / ve + (ve == 2 ? 1 : 0);
-      int x0 = rj / he - (he == 2 ? 1 : 0), x1 = (rj + rw - 1) / he + (he == 2 ? 1 : 0);
+      const int he = G.he[c], ve = G.ve[c], hsh = he >> 1, vsh = ve >> 1;  // 1 / 2 / 4 -> 0 / 1 / 2
+      int y0 = ((ri + r0) >> vsh) - (ve == 2 ? 1 : 0), y1 = ((ri + r1) >> vsh) + (ve == 2 ? 1 : 0);
+      int x0 = (rj >> hsh) - (he == 2 ? 1 : 0), x1 = ((rj + rw - 1) >> hsh) + (he == 2 ? 1 : 0);
       y0 = max(y0, 0);
       x0 = max(x0, 0);
       y1 = min(y1, G.ch[c] - 1);
@@ -1965,7 +2009,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
     need += nrows * rw * 4;
     if (need <= K2_LDS) {
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
-      if (t < oy1 - oy0) rtab[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+      if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(taps[out_w + oy0 + t]) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
       TPlane tp[3];
       // tile staging: the first SU dwords per thread of every component are
       // loaded before any LDS write (one memory round trip, not one per
@@ -2036,8 +2080,15 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       const int tx = t % K2_COLS, sub = t / K2_COLS;
       if (tx >= out_w / 2) return;
       const int dx0 = 2 * tx;
-      const LinTap l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
-      const LinTap l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
+      LinTap l0, l1;
+      if (taps) {  // K1's table (flip applied): both columns in one 16-byte load
+        const uint4 q = *(const uint4 *)(taps + dx0);
+        l0 = tap_unpack(make_uint2(q.x, q.y));
+        l1 = tap_unpack(make_uint2(q.z, q.w));
+      } else {
+        l0 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0));
+        l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
+      }
       // a border tap (src[s] * 2048) as the same two-tap form with weights
       // (2048, 0) on (s, s): branch-free, identical sums
       const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
@@ -2336,6 +2387,7 @@ struct ffcv_jpeg_ctx {
   uint64_t arena_bytes;
   unsigned long long *arena_top;
   ImgInfo *info;
+  uint2 *taps;
   uint8_t *gtab;
   uint64_t gtab_slot;
   uint32_t *eidx;  // entropy index (caller-owned), or NULL
@@ -2348,6 +2400,7 @@ static void free_ctx(ffcv_jpeg_ctx *c) {
   (void)hipFree(c->arena);
   (void)hipFree(c->arena_top);
   (void)hipFree(c->info);
+  (void)hipFree(c->taps);
   (void)hipFree(c->gtab);
   delete c;
 }
@@ -2383,6 +2436,7 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   if ((e = hipMalloc(&c->arena, c->arena_bytes)) != hipSuccess ||
       (e = hipMalloc(&c->arena_top, sizeof(unsigned long long))) != hipSuccess ||
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
+      (e = hipMalloc(&c->taps, sizeof(uint2) * K2_TAPS * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess) {
     int rc = ffcv::check_hip(e, "ffcv_jpeg_create: hipMalloc");
     free_ctx(c);
@@ -2442,6 +2496,7 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.arena_bytes = c->arena_bytes;
   a.arena_top = c->arena_top;
   a.info = c->info;
+  a.taps = c->taps;
   a.eidx = c->eidx;
   a.eidx_n = c->eidx_n;
   a.gtab = c->gtab;

@@ -2093,7 +2093,11 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       // (2048, 0) on (s, s): branch-free, identical sums
       const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
       const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
-      // horizontal pass of crop row r for both columns: sat_s16(h >> 4) per channel
+      // horizontal pass of crop row r for both columns: sat_s16(h >> 4) per
+      // channel.  The saturations of this walk never act (so they are not
+      // computed): weights are in [0, 2048] with c0 + c1 <= 2049 (linear_coef
+      // rounds each), so 0 <= h >> 4 <= 255 * 2049 >> 4 = 32655 and the
+      // vertical sum m0 + m1 <= 32655 * 2049 >> 16 = 1020, (1020 + 2) >> 2 = 255.
       auto hrow = [&](int r, int H[6]) {
         const uint32_t *row = rgbx + __mul24(r - r0, rw);
         const uint32_t p0 = row[l0.s], q0 = row[s0b];
@@ -2102,8 +2106,8 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
         for (int c = 0; c < 3; c++) {
           const int a0 = (p0 >> (8 * c)) & 255, b0 = (q0 >> (8 * c)) & 255;
           const int a1 = (p1 >> (8 * c)) & 255, b1 = (q1 >> (8 * c)) & 255;
-          H[c] = sat_s16i((a0 * a0w + b0 * b0w) >> 4);
-          H[3 + c] = sat_s16i((a1 * a1w + b1 * b1w) >> 4);
+          H[c] = (a0 * a0w + b0 * b0w) >> 4;
+          H[3 + c] = (a1 * a1w + b1 * b1w) >> 4;
         }
       };
       const int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
@@ -2129,8 +2133,10 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
         int o[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
-          const int m0 = __mul24(HA[i], ly.c0) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;  // |HA| < 2^15, c <= 2048
-          o[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
+          // (sat_s16(m0 + m1) + 2) >> 2 with the + 2 folded into m0 (2 << 16 is a
+          // multiple of 2^16), no saturation (see hrow)
+          const int m0 = (__mul24(HA[i], ly.c0) + (2 << 16)) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;
+          o[i] = (m0 + m1) >> 2;
         }
         if (ep.in_cut(dy, dx0)) {
           o[0] = ep.fill[0];

@@ -243,13 +243,18 @@ __global__ void __launch_bounds__(RRC_THREADS)
       wa[j] = l.border ? 2048 : l.c0;
       wb[j] = l.border ? 0 : l.c1;
     }
-    auto hrow = [&](int r, int H[12]) {  // resize.cpp HResizeLinear of crop row r: sat_s16(h >> 4)
+    // resize.cpp HResizeLinear of crop row r: sat_s16(h >> 4).  The
+    // saturations of this walk never act (so they are not computed): weights
+    // are in [0, 2048] with wa + wb <= 2049 (linear_coef rounds each), so
+    // 0 <= h >> 4 <= 255 * 2049 >> 4 = 32655 and the vertical sum
+    // m0 + m1 <= 32655 * 2049 >> 16 = 1020, (1020 + 2) >> 2 = 255.
+    auto hrow = [&](int r, int H[12]) {
       const uint8_t *row = L.row(r);
 #pragma unroll
       for (int j = 0; j < 4; j++)
 #pragma unroll
         for (int c = 0; c < 3; c++)
-          H[3 * j + c] = sat_s16i((row[xa[j] + c] * wa[j] + row[xb[j] + c] * wb[j]) >> 4);
+          H[3 * j + c] = (row[xa[j] + c] * wa[j] + row[xb[j] + c] * wb[j]) >> 4;
     };
     int ca = -1, cb = -1;
     int HA[12], HB[12];
@@ -271,9 +276,9 @@ __global__ void __launch_bounds__(RRC_THREADS)
       }
       int v[12];
 #pragma unroll
-      for (int i = 0; i < 12; i++) {  // VResizeLinearVec_32s8u
-        const int m0 = __mul24(HA[i], ly.c0) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;  // |HA| < 2^15, c <= 2048
-        v[i] = sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
+      for (int i = 0; i < 12; i++) {  // VResizeLinearVec_32s8u, + 2 folded into m0, no saturation (see hrow)
+        const int m0 = (__mul24(HA[i], ly.c0) + (2 << 16)) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;
+        v[i] = (m0 + m1) >> 2;
       }
       put(dy, v);
     }

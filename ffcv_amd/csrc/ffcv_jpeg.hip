@@ -2006,7 +2006,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       need += trows[c] * tpitch[c];
     }
     const int rgb_off = need;
-    need += nrows * rw * 4;
+    need += nrows * rw * 4 + 4;  // + a dummy word for the colour pass's off-crop pixels
     if (need <= K2_LDS) {
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
       if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(taps[out_w + oy0 + t]) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
@@ -2047,25 +2047,76 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       if (a.k2flags & 256) {
       } else if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
           G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {
-        // 4:2:0: one thread per chroma sample, its 2x2 pixel quad
-        const int R0 = Y0 >> 1, C0 = X0 >> 1, qcols = (X1 >> 1) - C0 + 1;
-        const int nq = ((Y1 >> 1) - R0 + 1) * qcols;
-        // i / qcols by a float reciprocal: exact while the quotient's
-        // rounding margin 0.5 / qcols exceeds its float error (qcols and
-        // i / qcols well below 2^11 here)
-        const float rq = 1.0f / (float)qcols;
-        for (int i = t; i < nq; i += K2T) {
-          const int qr = (int)(((float)i + 0.5f) * rq), R = R0 + qr, C = C0 + (i - __mul24(qr, qcols));
-          int cb[4], cr[4];
-          upsample_quad_h2v2(tp[1], G.cw[1], G.ch[1], R, C, cb);
-          upsample_quad_h2v2(tp[2], G.cw[2], G.ch[2], R, C, cr);
+        // 4:2:0 (jdsample.c h2v2_fancy_upsample, as upsample_quad_h2v2): each
+        // thread owns a pair of adjacent chroma columns (C, C + 1) and walks
+        // every ng-th chroma row of the band.  Column clamps, edge terms and
+        // offsets are computed once per thread; per row the 3 x 4 chroma
+        // neighbourhood of the two quads is read once per plane and its
+        // vertical sums (3 * centre + above / below) are shared by both quads.
+        // Pixels outside the crop go to a dummy LDS word (branch-free).
+        const int R0 = Y0 >> 1, R1 = Y1 >> 1, C0 = X0 >> 1, C1 = X1 >> 1;
+        const int npairs = (C1 - C0 + 2) >> 1;
+        const int ps = min(npairs, K2T);  // pairs per sweep of the workgroup
+        const float rp = 1.0f / (float)ps;
+        // ng row groups; t = g * ps + pair (quotients by a float reciprocal:
+        // exact for these small operands, as in the tile staging)
+        const int ng = (int)(((float)K2T + 0.5f) * rp);
+        const int g = (int)(((float)t + 0.5f) * rp);
+        if (g < ng)
+        for (int pr = t - __mul24(g, ps); pr < npairs; pr += ps) {
+          const int C = C0 + 2 * pr;
+          // plane columns of the two quads' neighbourhoods (clamped like
+          // upsample_quad_h2v2; the fourth is unused without a second quad)
+          const int cw = G.cw[1], ch = G.ch[1];
+          const int xm = max(C - 1, 0) - tp[1].c0, x0 = C - tp[1].c0;
+          const int x1 = min(C + 1, cw - 1) - tp[1].c0, x2 = min(C + 2, min(C1 + 1, cw - 1)) - tp[1].c0;
+          // luma columns 2C .. 2C + 3: inside the crop?  (reads clamped into it)
+          const int X = 2 * C;
+          bool vx[4];
+          int lx[4];
 #pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const int Y = 2 * R + (u >> 1), X = 2 * C + (u & 1);
-            if (Y < Y0 || Y > Y1 || X < X0 || X > X1) continue;
-            int v[3];
-            ycc_rgb(tp[0].at(Y, X), cb[u], cr[u], v);
-            rgbx[__mul24(Y - Y0, rw) + (X - X0)] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
+          for (int j = 0; j < 4; j++) {
+            vx[j] = X + j >= X0 && X + j <= X1;
+            lx[j] = min(max(X + j, X0), X1) - tp[0].c0;
+          }
+          uint32_t *dummy = rgbx + nrows * rw;
+          for (int R = R0 + g; R <= R1; R += ng) {
+            const int ru = max(R - 1, 0), rd = min(R + 1, ch - 1);
+            int qb[2][8];  // [plane][quad u: C's q0..q3, then C + 1's]
+#pragma unroll
+            for (int pl = 0; pl < 2; pl++) {
+              const uint8_t *b = tp[1 + pl].p;
+              const int pitch = tp[1 + pl].pitch, ty = tp[1 + pl].r0;
+              const uint8_t *rm = b + __mul24(R - ty, pitch), *ra = b + __mul24(ru - ty, pitch),
+                            *rb = b + __mul24(rd - ty, pitch);
+              const int mm = rm[xm], m0 = rm[x0], m1 = rm[x1], m2 = rm[x2];
+              // vertical sums above (T) and below (B) for columns xm, x0, x1, x2
+              const int Tm = 3 * mm + ra[xm], T0 = 3 * m0 + ra[x0], T1 = 3 * m1 + ra[x1], T2 = 3 * m2 + ra[x2];
+              const int Bm = 3 * mm + rb[xm], B0 = 3 * m0 + rb[x0], B1 = 3 * m1 + rb[x1], B2 = 3 * m2 + rb[x2];
+              qb[pl][0] = (3 * T0 + Tm + 8) >> 4;
+              qb[pl][1] = (3 * T0 + T1 + 7) >> 4;
+              qb[pl][2] = (3 * B0 + Bm + 8) >> 4;
+              qb[pl][3] = (3 * B0 + B1 + 7) >> 4;
+              qb[pl][4] = (3 * T1 + T0 + 8) >> 4;
+              qb[pl][5] = (3 * T1 + T2 + 7) >> 4;
+              qb[pl][6] = (3 * B1 + B0 + 8) >> 4;
+              qb[pl][7] = (3 * B1 + B2 + 7) >> 4;
+            }
+#pragma unroll
+            for (int dy = 0; dy < 2; dy++) {
+              const int Y = 2 * R + dy;
+              const bool vy = Y >= Y0 && Y <= Y1;
+              const uint8_t *ly = tp[0].p + __mul24(min(max(Y, Y0), Y1) - tp[0].r0, tp[0].pitch);
+              uint32_t *orow = rgbx + __mul24(Y - Y0, rw) - X0;
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const int u = (j >> 1) * 4 + dy * 2 + (j & 1);  // quad, then its q index
+                int v[3];
+                ycc_rgb(ly[lx[j]], qb[0][u], qb[1][u], v);
+                uint32_t *d = vy && vx[j] ? orow + X + j : dummy;
+                *d = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
+              }
+            }
           }
         }
       } else {

@@ -344,6 +344,37 @@ def test_jpeg_rrc_matches_oracle(hip_lib, oracle):
         assert bad.size == 0, f'samples {bad[:8]} differ'
 
 
+def test_jpeg_rrc_edge_crops(hip_lib, oracle):
+    """K2's 4:2:0 colour pass on crops at odd offsets and plane edges (odd
+    widths and heights), and on crops wider than one workgroup sweep of
+    chroma column pairs (a 16 x 1200 image cropped whole: 600 pairs)."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(77)
+    shapes = [(16, 1200), (16, 1200), (37, 301), (37, 301), (37, 301), (64, 65), (9, 700)]
+    imgs = [natural_image(rng, h, w) for h, w in shapes]
+    blobs = [encode_jpeg(im, 90, '4:2:0') for im in imgs]
+    crops = np.array([[0, 0, 16, 1200], [3, 5, 11, 1193], [0, 0, 37, 301], [1, 3, 35, 297],
+                      [5, 150, 31, 151], [0, 1, 63, 64], [2, 7, 7, 693]], np.int32)
+    B = len(imgs)
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    dec = L.JpegDecoder(B, max(h for h, _ in shapes), max(w for _, w in shapes), max(len(b) for b in blobs))
+    u8 = oracle.rrc_batch([(b, h, w, 0) for b, (h, w) in zip(blobs, shapes)], crops, 224, 224)
+    flips = (np.arange(B) % 2).astype(np.uint8)
+    p = L.RRCParams()
+    p.out_h, p.out_w = 224, 224
+    out = torch.zeros((B, 224, 224, 3), dtype=torch.uint8, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.rrc(d_buf, d_smp, B, torch.from_numpy(crops).to('cuda:0'), None, torch.from_numpy(flips).to('cuda:0'),
+            p, out, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    want = _oracle_post(u8, flips)
+    got = out.cpu().numpy()
+    bad = np.argwhere((got != want).reshape(B, -1).any(1)).ravel()
+    assert bad.size == 0, f'samples {bad} differ'
+
+
 def test_jpeg_corrupt_and_unsupported(hip_lib, oracle):
     torch = _torch()
     from ffcv_amd import libffcv as L

@@ -1184,12 +1184,31 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
 
 // P3-P5 with table set T (the workgroup's LDS copy or the image's global
 // copy; separate instantiations so each reads its own address space).
-// Entropy index record of one sample: EIDX_WORDS words per lane range,
-// [pos, z | ph << 8, first block], and lane 0's second word carries
-// EIDX_VALID | nthr << 16 once the whole record is published.
+// Entropy index record of one sample: EIDX_WORDS words per lane range t >= 1,
+// [pos, z | ph << 8, first block].  Lane 0's range always starts at (0, 0, 0),
+// so its words carry [hash high, EIDX_VALID | nthr << 16, hash low]: a 64-bit
+// hash of the other lanes' words.  Records are written and read with plain
+// memory operations and no fences (an agent-scope release / acquire writes
+// back / invalidates the whole L2 of the XCD): a record is used only when its
+// hash matches, so a reader that sees part of a record being published by a
+// concurrent launch on another XCD (lines not yet written back) decodes the
+// sample in full instead.  A record's content is a pure function of the
+// sample, so every publish writes the same words.
 #define EIDX_LANES 64
 #define EIDX_WORDS 3
 #define EIDX_VALID 0x80000000u
+FFCV_DEV uint64_t eidx_hash(uint32_t w0, uint32_t w1, uint32_t w2, int t) {
+  // per lane mix, then an xor over the wave (wave-uniform result)
+  uint64_t h = ((uint64_t)w0 << 32 | w1) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)w2 << 32 | (uint32_t)t) * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    lo ^= (uint32_t)__shfl_xor((int)lo, m);
+    hi ^= (uint32_t)__shfl_xor((int)hi, m);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
 template <class TB>
 FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, int sg, const uint32_t *words,
                              uint32_t total_bits, int16_t *coef, int16_t *dcd, uint64_t sample_id) {
@@ -1202,23 +1221,24 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   uint32_t *rec = nullptr;
   if (a.eidx && JL == EIDX_LANES && sample_id < a.eidx_n) rec = a.eidx + sample_id * (EIDX_LANES * EIDX_WORDS);
   if (rec) {
-    uint32_t head = 0;
-    if (t == 0) head = __hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    head = __builtin_amdgcn_readfirstlane(head);
-    if ((head & EIDX_VALID) && ((head >> 16) & 0xff) == nthr) {
-      // published by an earlier decode of this sample: acquire, then every
-      // lane starts from its exact state (no sync rounds, no block scan)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t w0 = __builtin_nontemporal_load(rec + EIDX_WORDS * t);
+    const uint32_t w1 = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 1);
+    const uint32_t w2 = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 2);
+    const uint32_t head = __builtin_amdgcn_readfirstlane(w1);
+    const uint64_t want = ((uint64_t)__builtin_amdgcn_readfirstlane(w0) << 32) | __builtin_amdgcn_readfirstlane(w2);
+    const uint64_t got = eidx_hash(t ? w0 : 0u, t ? w1 : 0u, t ? w2 : 0u, t);
+    if ((head & EIDX_VALID) && ((head >> 16) & 0xff) == nthr && wuni((uint32_t)(got == want))) {
+      // published by an earlier decode of this sample: every lane starts
+      // from its exact state (no sync rounds, no block scan)
       STAMP(3);
       STAMP(4);
       STAMP(5);
       if (active) {
         DecState g;
-        g.pos = __builtin_nontemporal_load(rec + EIDX_WORDS * t);
-        const uint32_t zp = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 1) & 0xffffu;
-        g.z = (int)(zp & 0xff);
-        g.ph = (int)(zp >> 8);
-        const uint32_t cur = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 2);
+        g.pos = t ? w0 : 0u;
+        g.z = t ? (int)(w1 & 0xff) : 0;
+        g.ph = t ? (int)((w1 >> 8) & 0xff) : 0;
+        const uint32_t cur = t ? w2 : 0u;
         uint32_t it_lane2 = 0;
         if (g.pos < my_end)
           write_range(S, T, words, wuni(S.ds_bytes), g, my_end, cur, wave_uniform((gshort_t *)coef),
@@ -1281,16 +1301,18 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   }
   const bool any_bad = seg_any(bad_lane, sg);
   if (rec && !any_bad) {  // publish this sample's converged lane states
-    if (active) {
-      const int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
-      rec[EIDX_WORDS * t] = g.pos;
-      if (t > 0) rec[EIDX_WORDS * t + 1] = (uint32_t)g.z | ((uint32_t)g.ph << 8);
-      rec[EIDX_WORDS * t + 2] = (uint32_t)cur;
+    const int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
+    uint32_t w0 = active ? g.pos : 0u, w1 = active ? (uint32_t)g.z | ((uint32_t)g.ph << 8) : 0u,
+             w2 = active ? (uint32_t)cur : 0u;
+    const uint64_t h = eidx_hash(t ? w0 : 0u, t ? w1 : 0u, t ? w2 : 0u, t);
+    if (t == 0) {  // lane 0's state is (0, 0, 0): its words carry the header and hash
+      w0 = (uint32_t)(h >> 32);
+      w1 = EIDX_VALID | (nthr << 16);
+      w2 = (uint32_t)h;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the record before its header
-    if (t == 0)
-      __hip_atomic_store(rec + 1, (uint32_t)g.z | ((uint32_t)g.ph << 8) | (nthr << 16) | EIDX_VALID, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    rec[EIDX_WORDS * t] = w0;
+    rec[EIDX_WORDS * t + 1] = w1;
+    rec[EIDX_WORDS * t + 2] = w2;
   }
 
   // ------------------------------------------------------------- P5 ----

@@ -9,7 +9,7 @@
 # launch so every launch has the same size (tools/pmc_summary.py divides by it).
 set -e
 TAG=${1:-r2}; shift || true
-ARGS="${@:---steps 48 --warmup 12 --no-cpu-baseline} --no-host-check"
+ARGS="${@:---steps 48 --warmup 12 --no-cpu-baseline} --no-host-check --no-later-epochs"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -191,7 +191,7 @@ struct JShared {
   // as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
   int4 pdesc[10][2];
   int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
-  int qmax[3];  // max |qmul| per component (the IDCT's 32-bit-product test)
+  int qmax[3];  // max |qmul| of the AC multipliers per component (the IDCT's 32-bit-product test)
   union {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
     uint32_t ev[2][NEV + 1][JL];  // P3: block-start events (pos << 4 | phase), double-buffered
@@ -661,9 +661,12 @@ FFCV_DEV uint8_t idct_rl(int x) {
   return (uint8_t)(u >= 640u ? 0u : min(u, 255u));
 }
 // jidctfst.c MULTIPLY: DESCALE(var * const, CONST_BITS = 8) with a JLONG
-// (64-bit) product.  The 32-bit form is identical whenever the product fits,
-// which holds for every dequantised input below 2^14 in magnitude (all valid
-// 8-bit baseline data); WIDE keeps the exact 64-bit form for the rest.
+// (64-bit) product.  The 32-bit form is identical whenever the product fits.
+// Interval bounds through jpeg_idct_ifast with every dequantised input
+// |d| <= M: pass-1 outputs <= 35.83 M (+ 5 from truncation), and the largest
+// product is pass 2's (z10 + z12) * 473 <= 67,787 M, below 2^31 for
+// M <= 31,680 (tools/idct_bound.py); the 32-bit form is used for M <= 30,000
+// and WIDE keeps the exact 64-bit form for the rest.
 template <bool WIDE>
 FFCV_DEV int fmul8(int v, int c) {
   return WIDE ? (int)(((int64_t)v * c) >> 8) : (v * c) >> 8;
@@ -737,20 +740,25 @@ FFCV_DEV void idct_block(const int16_t *cp, const int16_t *qm, int qmax, uint8_t
   int d[64];
 #pragma unroll
   for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
-  // max |coefficient| on packed halves (|-32768| reads as 32768 unsigned);
-  // max|coef| * max|qmul| < 2^14 bounds every dequantised input, so the
-  // 32-bit IDCT products are exact (else the exact 64-bit form runs)
+  // max |AC coefficient| on packed halves (|-32768| reads as 32768
+  // unsigned); max(|DC| * |qmul[0]|, max|AC| * max|AC qmul|) bounds every
+  // dequantised input (the DC term is the large one: a bright block's DC
+  // times the small DC multiplier), which selects the 32-bit IDCT products
+  // when they are exact (see fmul8)
   u16x2 mu = {0, 0};
 #pragma unroll
   for (int w = 0; w < 32; w++) {
-    const s16x2 v = *(const s16x2 *)(zz + 2 * w);
+    s16x2 v = *(const s16x2 *)(zz + 2 * w);
+    if (w == 0) v.x = 0;  // the DC coefficient
     const s16x2 av = __builtin_elementwise_max(v, (s16x2){0, 0} - v);
     mu = __builtin_elementwise_max(mu, __builtin_bit_cast(u16x2, av));
   }
   const int cmax = max((int)mu.x, (int)mu.y);
+  const int dc = zz[0], qdc = qm[0];
+  const int bound = max(abs(dc) * abs(qdc), cmax * qmax);
 #pragma unroll
   for (int n = 0; n < 64; n++) d[n] = (int)zz[kZigzagOfNatural[n]] * (int)qm[n];
-  if (cmax * qmax < (1 << 14))
+  if (bound <= 30000)
     idct_ifast_block<false>(d, out, stride);
   else
     idct_ifast_block<true>(d, out, stride);
@@ -1512,7 +1520,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     int n = c_natural[zz];
     const int16_t qmv = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
     S.qmul[c][n] = qmv;
-    atomicMax(&S.qmax[c], qmv < 0 ? -(int)qmv : (int)qmv);
+    if (n != 0) atomicMax(&S.qmax[c], qmv < 0 ? -(int)qmv : (int)qmv);
   }
   wsync_lds();  // header bytes are dead from here (P2 stages into the same LDS)
   if (match ? KS.tab.bad : gt->bad) {

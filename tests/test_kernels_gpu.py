@@ -249,6 +249,40 @@ def test_jpeg_full_decode_matches_libjpeg(hip_lib, oracle):
             assert np.array_equal(want, oracle.ljt_decode(blobs[k]))
 
 
+def test_jpeg_full_decode_low_quality_wide_idct(hip_lib, oracle):
+    """Low qualities (quantisers up to 255) on high-contrast content: blocks
+    whose dequantised inputs exceed the 32-bit IDCT product bound take the
+    exact 64-bit form beside blocks that do not, in the same wave."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(5)
+    imgs, blobs = [], []
+    for k, q in enumerate([1, 2, 3, 5, 8, 12, 20, 1, 2, 4]):
+        h, w = int(rng.integers(40, 200)), int(rng.integers(40, 200))
+        img = natural_image(rng, h, w)
+        if k % 2:  # hard edges: large AC coefficients
+            img = np.where(img > 127, 255, 0).astype(np.uint8)
+        imgs.append(img)
+        blobs.append(encode_jpeg(img, q, ['4:2:0', '4:4:4'][k % 2]))
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    maxh = max(i.shape[0] for i in imgs)
+    maxw = max(i.shape[1] for i in imgs)
+    dec = L.JpegDecoder(B, maxh, maxw, max(len(b) for b in blobs))
+    stride = maxh * maxw * 3
+    out = torch.zeros(B * stride, dtype=torch.uint8, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.decode(d_buf, d_smp, B, out, stride, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    o = out.cpu().numpy()
+    for k in range(B):
+        assert st[k] == 0, (k, st[k])
+        h, w = imgs[k].shape[:2]
+        got = o[k * stride:k * stride + h * w * 3].reshape(h, w, 3)
+        assert np.array_equal(got, oracle.ljt_decode(blobs[k])), f'sample {k}'
+
+
 def test_jpeg_full_decode_large_images(hip_lib, oracle):
     """Multi-megapixel streams: long lane ranges (many refills per lane, a wide
     sync-event stride, several sync rounds), every subsampling, greyscale and

@@ -12,7 +12,11 @@ the bench generator) with ffcv_amd.writer.DatasetWriter, then iterates
 
 in four modes and prints one JSON line per mode:
   * device_cache   : the .beton is copied to HBM once; per batch only indices
-                     move (the bench.py workload, seen through the Loader)
+                     move (the bench.py workload, seen through the Loader);
+                     the Loader's default entropy index is filled by the
+                     warm-up epoch, so the timed epochs skip the sync rounds
+  * device_cache_noindex : the same with entropy_index=False (every epoch
+                     decodes like the first)
   * pcie_in        : device_cache=False: per batch the compressed byte ranges
                      are gathered from the mmap into pinned staging and copied
                      host -> device (hipMemcpyAsync) before decoding
@@ -48,7 +52,8 @@ def main():
     ap.add_argument('--epochs', type=int, default=2)
     ap.add_argument('--batch', type=int, default=512)
     ap.add_argument('--dir', default=None)
-    ap.add_argument('--modes', default='link,device_cache,pcie_in,pcie_in_out,pcie_in_process_cache')
+    ap.add_argument('--modes', default='link,device_cache,device_cache_noindex,pcie_in,pcie_in_out,'
+                                       'pcie_in_process_cache')
     args = ap.parse_args()
 
     import torch
@@ -84,7 +89,8 @@ def main():
             print(json.dumps(link_rates(torch, dev, args.batch * 224 * 224 * 3 * 2)), flush=True)
             continue
         loader = Loader(fn, batch_size=args.batch, order=OrderOption.RANDOM, seed=0, drop_last=True,
-                        device=dev, device_cache=(mode == 'device_cache'),
+                        device=dev, device_cache=mode.startswith('device_cache'),
+                        entropy_index=(mode != 'device_cache_noindex'),
                         os_cache=(mode != 'pcie_in_process_cache'),
                         pipelines={'image': [RandomResizedCropRGBImageDecoder((224, 224)),
                                              Cutout(32, (124, 116, 103)), ToTensor(), ToDevice(dev),

@@ -81,6 +81,10 @@
 #define STAGE_BYTES (DS_FLUSH * JL * 4 + 64)  // a flush's bytes + the carried tail + pad
 #define STAGE_DUMMY (STAGE_BYTES - 4)
 #define STREAM_PAD 32   // zero bytes after the de-stuffed stream
+#ifndef ACS_Z
+#define ACS_Z 24        // zigzag positions of a block the write pass stages in LDS
+#endif
+#define ACS_BYTES (ACS_Z * 2)
 #ifndef BAND
 #define BAND 16  // K2 output rows per workgroup
 #endif
@@ -192,10 +196,11 @@ struct JShared {
   int4 pdesc[10][2];
   int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
   int qmax[3];  // max |qmul| of the AC multipliers per component (the IDCT's 32-bit-product test)
-  union {
+  union __attribute__((aligned(16))) {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
     uint32_t ev[2][NEV + 1][JL];  // P3: block-start events (pos << 4 | phase), double-buffered
     uint8_t stage[STAGE_BYTES];   // P2: de-stuffed bytes awaiting a flush
+    uint4 acs[JL][ACS_BYTES / 16];  // P5: each lane's block of low-frequency AC coefficients
   };
 };
 
@@ -529,11 +534,29 @@ FFCV_DEV int huff_value(uint32_t w, uint32_t off, uint32_t s) {
 }
 
 typedef __attribute__((address_space(1))) int16_t gshort_t;  // global memory
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
+// Coefficient stores.  A 2-byte store per non-zero coefficient, scattered
+// over the window's blocks, cost ~23% of this kernel (measured without them),
+// about in proportion to the lanes that store.  So the AC coefficients at
+// zigzag positions below ACS_Z (most of a block's non-zero ones) collect in
+// the lane's LDS slot (the event area, dead after the sync pass) and leave as
+// three 16-byte stores when the block ends; the rest, and the blocks a lane
+// shares with its neighbour (the one it starts inside, the one it stops
+// inside: their positions below the split belong to one lane each), are
+// stored directly.  The window coefficients were zeroed before this pass, so
+// unwritten positions read as zero either way.  Every step issues the same
+// vector memory instructions (out-of-range offsets where a lane has nothing
+// to store), so the refill waits on a static vmcnt.
 template <class TB>
 FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32_t words_bytes, DecState st,
                           uint32_t end_bit, uint32_t blk, gshort_t *coef, uint32_t coef_bytes, gshort_t *dcd,
                           uint32_t dcd_bytes, uint32_t &iters) {
+  uint4 *acs = S.acs[threadIdx.x % JL];
+  int16_t *acs16 = (int16_t *)acs;
+#pragma unroll
+  for (int q = 0; q < ACS_BYTES / 16; q++) acs[q] = make_uint4(0, 0, 0, 0);
+  bool stg = st.z == 0;  // a block entered part-way is the previous lane's to stage
   BufReader br;
   br.init(words, words_bytes, st.pos);
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)coef, 0, (int)coef_bytes, BUF_CFG);
@@ -572,14 +595,43 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     // second AC coefficient, each out of range when the lane has none
 #ifndef K1_TIMING_NOSTORE
     const uint32_t o1 = (boff + (uint32_t)min(z + zinc - 1, 63)) * 2, o2 = (boff + (uint32_t)min(z + zadd - 1, 63)) * 2;
+#ifndef K1_TIMING_NODC
     __builtin_amdgcn_raw_buffer_store_b16((short)v, drs, isblk ? blk * 2 : BUF_OOR, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, !isblk && size && inwin ? o1 : BUF_OOR, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, size2 && inwin ? o2 : BUF_OOR, 0, 0);
+#endif
+#ifndef K1_TIMING_NOAC
+    const int p1 = min(z + zinc - 1, 63), p2 = min(z + zadd - 1, 63);
+    const bool a1 = !isblk && size && inwin, a2 = size2 && inwin;
+    const bool l1 = a1 && stg && p1 < ACS_Z, l2 = a2 && stg && p2 < ACS_Z;
+    if (l1) acs16[p1] = (int16_t)v;
+    if (l2) acs16[p2] = (int16_t)v2;
+    __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, a1 && !l1 ? o1 : BUF_OOR, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, a2 && !l2 ? o2 : BUF_OOR, 0, 0);
+#endif
 #else  // timing only (wrong output): the write pass without its stores
     if (v == 0x7fffffff && v2 == 0x7fffffff) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, boff, 0, 0);
 #endif
     z += zadd;
     const bool bend = z >= 64;
+#ifndef K1_TIMING_NOAC
+    {  // a staged block that ends leaves as three 16-byte stores
+      const bool fl = bend && stg && inwin;
+      uint4 c[ACS_BYTES / 16];
+#pragma unroll
+      for (int q = 0; q < ACS_BYTES / 16; q++) c[q] = make_uint4(0, 0, 0, 0);
+      if (fl) {
+#pragma unroll
+        for (int q = 0; q < ACS_BYTES / 16; q++) {
+          c[q] = acs[q];
+          acs[q] = make_uint4(0, 0, 0, 0);
+        }
+      }
+      const uint32_t fo = fl ? boff * 2 : BUF_OOR;
+#pragma unroll
+      for (int q = 0; q < ACS_BYTES / 16; q++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, c[q]), crs, fo + 16 * q, 0, 0);
+    }
+    stg = stg || bend;
+#endif
     // the next block: (blk + 1, nph, mx', my')
     const bool wrap = nph == 0;
     const int nmx = wrap ? (mx + 1 == mcux ? 0 : mx + 1) : mx;
@@ -597,6 +649,14 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     boff = bend ? nboff : boff;
     inwin = bend ? ninwin : inwin;
   }
+#ifndef K1_TIMING_NOAC
+  if (stg && z > 0 && inwin) {  // stopped inside a staged block: its positions below z are this lane's
+    for (int q = 0; q < ACS_Z; q++) {
+      const int c = acs16[q];
+      if (q < z && c != 0) __builtin_amdgcn_raw_buffer_store_b16((short)c, crs, (boff + (uint32_t)q) * 2, 0, 0);
+    }
+  }
+#endif
 }
 
 // Cross-lane helpers on DPP (no LDS round trip, unlike __shfl's
@@ -1217,6 +1277,17 @@ FFCV_DEV uint64_t eidx_hash(uint32_t w0, uint32_t w1, uint32_t w2, int t) {
   }
   return ((uint64_t)hi << 32) | lo;
 }
+// Zero the image's window coefficients right before the write pass stores
+// its non-zero ones: the lines are then still in L2 when the scattered 2-byte
+// stores and the IDCT's block reads reach them (zeroed at allocation, ~300 us
+// earlier, they had been written back and the stores missed).
+FFCV_DEV void zero_window_coefs(const JShared &S, int16_t *coef, int t) {
+  uint4 *cz = wave_uniform((uint4 *)coef);
+  const uint32_t n = wuni((uint32_t)(S.nwin * 8));
+  for (uint32_t i = (uint32_t)t; i < n; i += JL) cz[i] = make_uint4(0, 0, 0, 0);
+  wsync_mem();
+}
+
 template <class TB>
 FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, int sg, const uint32_t *words,
                              uint32_t total_bits, int16_t *coef, int16_t *dcd, uint64_t sample_id) {
@@ -1241,6 +1312,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
       STAMP(3);
       STAMP(4);
       STAMP(5);
+      zero_window_coefs(S, coef, t);
       if (active) {
         DecState g;
         g.pos = t ? w0 : 0u;
@@ -1325,6 +1397,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 
   // ------------------------------------------------------------- P5 ----
   STAMP(5);
+  zero_window_coefs(S, coef, t);
   uint32_t it_lane2 = 0;
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
@@ -1370,8 +1443,6 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
     S.poff[c] = o - ((uint64_t)S.wy0[c] * 8 * wstride + (uint64_t)S.wx0[c] * 8);  // wraps: see ImgInfo
     o += wstride * (uint64_t)(S.wy1[c] - S.wy0[c] + 1) * 8;
   }
-  uint4 *cz = (uint4 *)(a.arena + S.cf_off);
-  for (uint32_t i = (uint32_t)t; i < (uint32_t)(S.nwin * 8); i += JL) cz[i] = make_uint4(0, 0, 0, 0);
   return FFCV_SAMPLE_OK;
 }
 

@@ -501,10 +501,16 @@ def main():
     pm = load_profile(f'traffic_{args.config}.json')
     if pm and all(n in pm and 'fetch_size_kb' in pm[n] and 'write_size_kb' in pm[n] and 'images' in pm[n]
                   for n in kernels):
-        per_img = sum((pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 / pm[n]['images'] for n in kernels)
+        # gfx950 FETCH_SIZE counts 64 B per 128-B request of 16-byte-per-lane
+        # streaming loads (MI355X_MICROARCH.md, HBM): the raw kernel stages
+        # with uint4 loads, so its fetch counts half its bytes
+        fx = {n: 2.0 if n.startswith('rrc_raw_kernel') else 1.0 for n in kernels}
+        per_img = sum((pm[n]['fetch_size_kb'] * fx[n] + pm[n]['write_size_kb']) * 1024.0 / pm[n]['images']
+                      for n in kernels)
         hbm['traffic'] = round(per_img * imgs_per_launch, 1)
         hbm['traffic_per_image'] = round(per_img, 1)
-        hbm['traffic_note'] = (f'HBM bytes per launch of {imgs_per_launch:.0f} images (FETCH_SIZE + WRITE_SIZE, '
+        hbm['traffic_note'] = (f'HBM bytes per launch of {imgs_per_launch:.0f} images (FETCH_SIZE'
+                               f'{" x2 (16-B loads, gfx950)" if mode != "jpg" else ""} + WRITE_SIZE, '
                                f'rocprofv3 PMC, profiles/traffic_{args.config}.json, build {pm.get("_build")}); '
                                f'algorithmic {unit_bytes * imgs_per_launch:.0f}')
     launch = {'kernel': ' + '.join(kernels) + f' (launches of {imgs_per_launch:.0f} images)',

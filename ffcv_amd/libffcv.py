@@ -314,7 +314,11 @@ def arena_for(heights, widths, nbytes, max_batch):
     b = scratch_bound(heights, widths, nbytes)
     if b.size > max_batch:
         b = np.partition(b, b.size - max_batch)[b.size - max_batch:]
-    return int(b.sum()) + 4096
+    # fewer images than a launch (repeated samples: a small dataset, padded
+    # distributed orders, replicated benchmark encodings): each extra slot
+    # may hold the largest image again
+    extra = max(0, max_batch - b.size) * (int(b.max()) if b.size else 0)
+    return int(b.sum()) + extra + 4096
 
 
 EIDX_LANES, EIDX_WORDS = 64, 3  # entropy index record: words per lane range

@@ -124,4 +124,5 @@ def test_scratch_bound_matches_c(hip_lib):
     for h, w, n, g in zip(hs, ws, ns, got):
         assert int(g) == L.lib().ffcv_jpeg_scratch_bound(int(h), int(w), int(n))
     assert L.arena_for(hs, ws, ns, 10) == int(np.sort(got)[-10:].sum()) + 4096
-    assert L.arena_for(hs[:5], ws[:5], ns[:5], 10) == int(got[:5].sum()) + 4096
+    # a launch of 10 from 5 images: the 5 extra slots may repeat the largest
+    assert L.arena_for(hs[:5], ws[:5], ns[:5], 10) == int(got[:5].sum() + 5 * got[:5].max()) + 4096

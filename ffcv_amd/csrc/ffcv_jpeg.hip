@@ -1304,7 +1304,8 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
     const uint32_t w1 = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 1);
     const uint32_t w2 = __builtin_nontemporal_load(rec + EIDX_WORDS * t + 2);
     const uint32_t head = __builtin_amdgcn_readfirstlane(w1);
-    const uint64_t want = ((uint64_t)__builtin_amdgcn_readfirstlane(w0) << 32) | __builtin_amdgcn_readfirstlane(w2);
+    const uint64_t want = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(w0) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(w2);
     const uint64_t got = eidx_hash(t ? w0 : 0u, t ? w1 : 0u, t ? w2 : 0u, t);
     if ((head & EIDX_VALID) && ((head >> 16) & 0xff) == nthr && wuni((uint32_t)(got == want))) {
       // published by an earlier decode of this sample: every lane starts
@@ -1312,6 +1313,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
       STAMP(3);
       STAMP(4);
       STAMP(5);
+      if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + 12] = ~0ull;  // index hit: no sync rounds
       zero_window_coefs(S, coef, t);
       if (active) {
         DecState g;
@@ -1426,8 +1428,10 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
   const uint64_t need = ds + cf + dc + pl + rgb;
   unsigned long long base = 0;
   if (t == 0) base = atomicAdd(a.arena_top, (unsigned long long)need);
-  base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
-         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+  // readfirstlane returns int: widen through uint32_t (an offset at or past
+  // 2^31 would otherwise sign-extend and read as TOO_LARGE)
+  base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
   if (base + need > a.arena_bytes) return FFCV_SAMPLE_TOO_LARGE;  // arena exhausted
   S.ds_off = base;
   S.ds_bytes = (uint32_t)ds;
@@ -2635,6 +2639,20 @@ int ffcv_jpeg_set_entropy_index(ffcv_jpeg_ctx *c, uint32_t *index, uint64_t n_sa
   }
   c->eidx = index;
   c->eidx_n = index ? n_samples : 0;
+  return FFCV_OK;
+}
+
+int ffcv_jpeg_arena_used(ffcv_jpeg_ctx *c, void *stream, uint64_t *used, uint64_t *capacity) {
+  if (!c || !used) {
+    ffcv::set_error("ffcv_jpeg_arena_used: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  unsigned long long v = 0;
+  hipStream_t s = ffcv::as_stream(stream);
+  FFCV_HIP_CHECK(hipMemcpyAsync(&v, c->arena_top, sizeof(v), hipMemcpyDeviceToHost, s));
+  FFCV_HIP_CHECK(hipStreamSynchronize(s));
+  *used = v;
+  if (capacity) *capacity = c->arena_bytes;
   return FFCV_OK;
 }
 

@@ -90,6 +90,7 @@ _SIGS = {
     'ffcv_jpeg_create_arena': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64, c_uint64]),
     'ffcv_jpeg_scratch_bound': (c_uint64, [c_uint32, c_uint32, c_uint64]),
     'ffcv_jpeg_set_diag': (c_int, [c_void_p, c_int, c_int]),
+    'ffcv_jpeg_arena_used': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'ffcv_jpeg_set_entropy_index': (c_int, [c_void_p, c_void_p, c_uint64]),
     'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -312,6 +313,8 @@ def arena_for(heights, widths, nbytes, max_batch):
     """Arena bytes that no launch of max_batch images of this dataset can
     exhaust: the sum of the max_batch largest per-image bounds."""
     b = scratch_bound(heights, widths, nbytes)
+    if max_batch <= 0:
+        return 4096
     if b.size > max_batch:
         b = np.partition(b, b.size - max_batch)[b.size - max_batch:]
     # fewer images than a launch (repeated samples: a small dataset, padded
@@ -363,6 +366,13 @@ class JpegDecoder:
         """Diagnostics: kernels a launch runs (bit 0 K1, bit 2 K2) and K2
         timing-only flags, fixed on this context (never read per launch)."""
         _check(lib().ffcv_jpeg_set_diag(self.handle, int(only), int(k2flags)), 'ffcv_jpeg_set_diag')
+
+    def arena_used(self, stream=None):
+        """(bytes the last entropy launch allocated, arena capacity)."""
+        used, cap = c_uint64(), c_uint64()
+        _check(lib().ffcv_jpeg_arena_used(self.handle, _stream(stream), ctypes.byref(used), ctypes.byref(cap)),
+               'ffcv_jpeg_arena_used')
+        return used.value, cap.value
 
     def set_entropy_index(self, index):
         """Attach (or, with None, detach) an entropy index: a zeroed uint32

@@ -213,6 +213,12 @@ uint64_t ffcv_jpeg_scratch_bound(uint32_t height, uint32_t width,
                                  uint64_t nbytes);
 int ffcv_jpeg_destroy(ffcv_jpeg_ctx *ctx);
 
+/* Arena bytes the last entropy launch on `stream` bump-allocated (waits for
+ * the stream), and the arena's capacity (may be NULL): the high-water mark
+ * for sizing arenas. */
+int ffcv_jpeg_arena_used(ffcv_jpeg_ctx *ctx, void *stream, uint64_t *used,
+                         uint64_t *capacity);
+
 /* rgb_image.py:185-210 jpg branch fused end to end: decode only the MCUs the
  * crop needs -> crop -> INTER_AREA -> cutout -> LUT.  Samples with mode !=
  * jpg are skipped (call ffcv_rrc_raw_batch for them).  status: device

@@ -283,6 +283,33 @@ def test_jpeg_full_decode_low_quality_wide_idct(hip_lib, oracle):
         assert np.array_equal(got, oracle.ljt_decode(blobs[k])), f'sample {k}'
 
 
+def test_jpeg_launch_arena_past_2g(hip_lib, oracle):
+    """One launch whose bump-allocated scratch runs past 2^31 bytes of the
+    arena (240 decodes of a 1024x1024 4:4:4 stream, ~9.8 MB each): offsets
+    at or above 2^31 stay unsigned through the wave broadcast, so every
+    image decodes (they failed TOO_LARGE when the broadcast sign-extended)."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(77)
+    img = natural_image(rng, 1024, 1024)
+    blob = encode_jpeg(img, 90, '4:4:4')
+    B = 240
+    buf, offs, sizes = pack([blob])
+    smp = _samples(np.repeat(offs, B), np.repeat(sizes, B), [1024] * B, [1024] * B, np.zeros(B))
+    d_buf, d_smp = _upload(buf), _dev(smp)
+    dec = L.JpegDecoder(B, 1024, 1024, len(blob))
+    stride = 1024 * 1024 * 3
+    out = torch.zeros(B * stride, dtype=torch.uint8, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.decode(d_buf, d_smp, B, out, stride, status)
+    torch.cuda.synchronize()
+    used, cap = dec.arena_used()
+    assert 2 ** 31 < used <= cap, (used, cap)
+    assert (status.cpu().numpy() == 0).all(), np.nonzero(status.cpu().numpy())
+    ref = torch.from_numpy(oracle.ljt_decode(blob).reshape(-1)).to('cuda:0')
+    assert bool((out.view(B, stride) == ref).all())
+
+
 def test_jpeg_full_decode_large_images(hip_lib, oracle):
     """Multi-megapixel streams: long lane ranges (many refills per lane, a wide
     sync-event stride, several sync rounds), every subsampling, greyscale and
@@ -552,6 +579,22 @@ def test_jpeg_entropy_index(hip_lib, oracle):
     for (po, ps), (xo, xs) in zip(plain, (first, second)):
         assert np.array_equal(ps, xs) and np.array_equal(po, xo)
     assert (first[1][:B - 1] == 0).sum() == n and first[1][-1] != 0
+    # every good sample takes the indexed path (debug slot 12 = ~0 marks a
+    # hit; a miss writes its sync-round count there): records whose hash has
+    # bit 31 set in either word must match too
+    import ctypes
+    lib = L.lib()
+    lib.ffcv_jpeg_set_debug.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    dbg = torch.zeros((B, 16), dtype=torch.int64, device='cuda:0')
+    lib.ffcv_jpeg_set_debug(dec.handle, ctypes.c_void_p(dbg.data_ptr()))
+    run(2)
+    lib.ffcv_jpeg_set_debug(dec.handle, None)
+    slot = dbg[:, 12].cpu().numpy()
+    good = ids < n - 1
+    assert (slot[good] == -1).all(), np.nonzero(slot[good] != -1)
+    lo = index[:, 0, 2].cpu().numpy().astype(np.uint32)
+    hi = index[:, 0, 0].cpu().numpy().astype(np.uint32)
+    assert ((lo[:n - 1] | hi[:n - 1]) >> 31).any()  # the sign-bit case is exercised
     dec.set_entropy_index(None)
     assert np.array_equal(run(1)[0], plain[1][0])
     with pytest.raises(ValueError):

@@ -59,12 +59,15 @@ WORKLOAD = {
     'c2': 'C2: 10k-JPEG .beton (synthetic 256px q90), RRC 224 u8, batch 256',
     'c5': 'C5: raw 512x512 RGB .beton, RRC 448 + Cutout(64) u8, batch 256',
 }
-# batches per launch and launches in flight (tools/sweep_group.sh):
+# batches per launch and launches in flight (tools/g_sweep*.sh):
 # a JPEG launch of >= 4,096 images fills K1's residency (4 WGs x 4 images per
-# CU); C3 6,144 images x 3 in flight measured best (2.43 M/s at 400 steps,
-# 2.30 M/s at the driver's 20); the raw kernel has 7,168 workgroups per batch
-# and groups only to cut host submissions
-GROUP = {'c3': 12, 'c2': 24, 'c5': 4}
+# CU); fewer, larger launches cut the per-launch tails (C3 at 400 steps: 2.62 M/s
+# with 12 batches per launch, 2.74 M/s with 20-32), but a job of K batches
+# keeps at least two launches so one's K1 overlaps the other's K2 (at the
+# driver's 20 steps: 2.48 M/s with 10-12, 2.33 M/s as one launch of 20); the
+# raw kernel has 7,168 workgroups per batch and groups only to cut host
+# submissions
+GROUP = {'c3': 24, 'c2': 24, 'c5': 4}
 INFLIGHT = {'c3': 3, 'c2': 3, 'c5': 3}
 IMAGENET_MEAN = np.array([0.485, 0.456, 0.406]) * 255
 IMAGENET_STD = np.array([0.229, 0.224, 0.225]) * 255
@@ -247,7 +250,7 @@ def main():
     mode, side, out, batch, cut, norm, default_n = CONFIGS[args.config]
     if args.batch:  # diagnostic: launch granularity (not the BASELINE config)
         batch = args.batch
-    G = max(1, args.group or GROUP[args.config])
+    G = max(1, args.group or min(GROUP[args.config], -(-args.steps // 2)))
     S = max(1, args.inflight or INFLIGHT[args.config])
     N = args.dataset_size or default_n
     workers = max(1, min(16, cpu_threads() // max(1, world)))

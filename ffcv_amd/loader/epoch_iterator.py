@@ -41,8 +41,9 @@ from ..pipeline import runtime
 from ..pipeline.compiler import Compiler
 from ..utils import chunks
 
-# samples per decode launch that fill the GPU (bench.py GROUP: 12 x 512)
-TARGET_LAUNCH_SAMPLES = 6144
+# samples per decode launch (bench.py GROUP: 24 x 512 measured best at 400
+# steps; launches of 6,144 lost ~5% to per-launch tails)
+TARGET_LAUNCH_SAMPLES = 12288
 MAX_GROUP = 32
 N_SETS = 3
 

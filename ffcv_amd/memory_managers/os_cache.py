@@ -1,6 +1,9 @@
-"""OS page-cache manager (ffcv/memory_managers/os_cache.py:13-61): the whole
-file is np.memmap'd; ``read(address, state)`` returns
-``mmap[address:address + sizes[searchsorted(ptrs, address)]]``."""
+"""OS page-cache manager (ffcv/memory_managers/os_cache.py:13-61).
+
+The .beton is mapped read-only once per context; a sample's bytes are the
+slice of the map that starts at its address and runs for the size of the
+allocation-table entry found by binary search over the sorted pointers.
+"""
 import numpy as np
 
 from .base import MemoryManager, MemoryContext
@@ -13,19 +16,21 @@ class OSCacheContext(MemoryContext):
 
     @property
     def state(self):
-        return (self.mmap, self.manager.ptrs, self.manager.sizes)
+        m = self.manager
+        return (self.mmap, m.ptrs, m.sizes)
 
     def __enter__(self):
-        res = super().__enter__()
-        if self.mmap is None:
-            self.mmap = np.memmap(self.manager.reader.file_name, 'uint8', mode='r')
-        return res
+        entered = super().__enter__()
+        if self.mmap is None:  # mapped lazily, kept across epochs
+            self.mmap = np.memmap(self.manager.reader.file_name, dtype=np.uint8, mode='r')
+        return entered
 
-    def __exit__(self, __exc_type, __exc_value, __traceback):
-        return super().__exit__(__exc_type, __exc_value, __traceback)
+    def __exit__(self, *exc):
+        return super().__exit__(*exc)
 
 
 class OSCacheManager(MemoryManager):
+    """Every epoch shares one context: the kernel's page cache does the work."""
 
     def __init__(self, reader):
         super().__init__(reader)
@@ -40,6 +45,7 @@ class OSCacheManager(MemoryManager):
 
     def compile_reader(self):
         def read(address, mem_state):
-            size = mem_state[2][np.searchsorted(mem_state[1], address)]
-            return mem_state[0][address:address + size]
+            mapped, ptrs, sizes = mem_state
+            entry = np.searchsorted(ptrs, address)
+            return mapped[address:address + sizes[entry]]
         return read

@@ -33,29 +33,20 @@ FieldDescType = np.dtype([
     ('arguments', ('<u1', (1024,)))
 ], align=True)
 
-TYPE_ID_HANDLER = {
-    255: None,
-    0: FloatField,
-    1: IntField,
-    2: RGBImageField,
-    3: BytesField,
-    4: NDArrayField,
-    5: JSONField,
-    6: TorchTensorField,
-}
+# type id -> field class (255: a slot without a field)
+_FIELD_CLASSES = (FloatField, IntField, RGBImageField, BytesField, NDArrayField,
+                  JSONField, TorchTensorField)
+TYPE_ID_HANDLER = {255: None, **dict(enumerate(_FIELD_CLASSES))}
 
 
 def get_handlers(field_descriptors):
-    handlers = []
-    for field_descriptor in field_descriptors:
-        type_id = field_descriptor['type_id']
-        Handler = TYPE_ID_HANDLER[type_id]
-        if Handler is None:
-            handlers.append(None)
-        else:
-            handlers.append(Handler.from_binary(field_descriptor['arguments']))
-    return handlers
+    """One decoded field handler per descriptor row (None for id 255)."""
+    def handler(desc):
+        cls = TYPE_ID_HANDLER[desc['type_id']]
+        return None if cls is None else cls.from_binary(desc['arguments'])
+    return [handler(d) for d in field_descriptors]
 
 
 def get_metadata_type(handlers: List[Field]) -> np.dtype:
-    return np.dtype([('', handler.metadata_type) for handler in handlers], align=True)
+    """Per-sample metadata record: the fields' metadata types, C-aligned."""
+    return np.dtype([('', h.metadata_type) for h in handlers], align=True)

@@ -843,7 +843,7 @@ struct JpegArgs {
   // scratch follows the content instead of dataset-max x batch.
   uint8_t *arena;
   uint64_t arena_bytes;
-  unsigned long long *arena_top;  // zeroed on the stream before each K1
+  unsigned long long *arena_top;  // [0] bump counter (0 when K1 starts), [1] last launch's high water
   ImgInfo *info;
   uint2 *taps;    // K2_TAPS packed linear taps per image (RRC), written by K1
   uint8_t *gtab;  // per-image JTables for images that cannot share the workgroup's
@@ -2009,6 +2009,13 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
   const int t = threadIdx.x;
   const int k = blockIdx.y;
   const int band = blockIdx.x;
+  if (k == 0 && band == 0 && t == 0) {  // K1 is done: close its arena (see arena_before_k1)
+    const unsigned long long top = a.arena_top[0];
+    if (top) {
+      a.arena_top[1] = top;
+      a.arena_top[0] = 0;
+    }
+  }
   const ImgInfo &I = a.info[k];
   const int status = I.status;
   if (status == -1) return;  // raw sample (handled by the raw kernel)
@@ -2547,7 +2554,8 @@ struct ffcv_jpeg_ctx {
   uint64_t max_bytes;
   uint8_t *arena;  // per-launch scratch, bump-allocated per image by K1
   uint64_t arena_bytes;
-  unsigned long long *arena_top;
+  unsigned long long *arena_top;  // [0] bump counter, [1] high water of the last launch K2 closed
+  bool arena_zero;  // [0] is 0 at the stream's tail: the last launch ran K2, which zeroes it
   ImgInfo *info;
   uint2 *taps;
   uint8_t *gtab;
@@ -2596,7 +2604,8 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   c->gtab_slot = align_up(sizeof(JTables), 256);
   hipError_t e;
   if ((e = hipMalloc(&c->arena, c->arena_bytes)) != hipSuccess ||
-      (e = hipMalloc(&c->arena_top, sizeof(unsigned long long))) != hipSuccess ||
+      (e = hipMalloc(&c->arena_top, 2 * sizeof(unsigned long long))) != hipSuccess ||
+      (e = hipMemset(c->arena_top, 0, 2 * sizeof(unsigned long long))) != hipSuccess ||
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->taps, sizeof(uint2) * K2_TAPS * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess) {
@@ -2604,6 +2613,7 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
     free_ctx(c);
     return rc;
   }
+  c->arena_zero = true;
   *out = c;
   return FFCV_OK;
 }
@@ -2647,11 +2657,11 @@ int ffcv_jpeg_arena_used(ffcv_jpeg_ctx *c, void *stream, uint64_t *used, uint64_
     ffcv::set_error("ffcv_jpeg_arena_used: invalid arguments");
     return FFCV_EINVAL;
   }
-  unsigned long long v = 0;
+  unsigned long long v[2] = {0, 0};
   hipStream_t s = ffcv::as_stream(stream);
-  FFCV_HIP_CHECK(hipMemcpyAsync(&v, c->arena_top, sizeof(v), hipMemcpyDeviceToHost, s));
+  FFCV_HIP_CHECK(hipMemcpyAsync(v, c->arena_top, sizeof(v), hipMemcpyDeviceToHost, s));
   FFCV_HIP_CHECK(hipStreamSynchronize(s));
-  *used = v;
+  *used = c->arena_zero ? v[1] : v[0];
   if (capacity) *capacity = c->arena_bytes;
   return FFCV_OK;
 }
@@ -2698,7 +2708,17 @@ static int check_common(const char *fn, ffcv_jpeg_ctx *c, const uint8_t *base, c
   return FFCV_OK;
 }
 
-static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void *out) {
+// The bump counter must be 0 when K1 starts.  K2 zeroes it (its first
+// workgroup, after K1 has finished on the stream), so a launch that follows
+// one with K2 needs no memset: a memset is a kernel, and queued behind another
+// stream's K1 it held this stream's K1 back by ~0.7 ms (rocprofv3 trace).
+static int arena_before_k1(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s) {
+  if (!c->arena_zero) FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), s));
+  c->arena_zero = false;
+  return FFCV_OK;
+}
+
+static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void *out) {
   const int batch = a.batch;
   a.p = *p;
   a.out = out;
@@ -2707,7 +2727,7 @@ static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void
   a.out_stride = p->out_stride ? p->out_stride : dense;
   const int only = a.diag_only;
   if (only & 1) {
-    FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), s));
+    if (int rc = arena_before_k1(c, a, s)) return rc;
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), K1_PAD,
                        s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
@@ -2719,6 +2739,7 @@ static int launch_rrc(JpegArgs &a, hipStream_t s, const ffcv_rrc_params *p, void
   else
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, false>), g2, dim3(K2T), K2_LDS, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<RRC>");
+  if (only & 4) c->arena_zero = true;
   return FFCV_OK;
 }
 
@@ -2736,7 +2757,7 @@ int ffcv_jpeg_rrc_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   a.crops = crops;
   a.cut = cutout_yx;
   a.flips = flips;
-  return launch_rrc(a, ffcv::as_stream(stream), p, out);
+  return launch_rrc(c, a, ffcv::as_stream(stream), p, out);
 }
 
 int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, const ffcv_sample *table,
@@ -2767,7 +2788,7 @@ int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, con
   a.crops = a.crops_w = crops;
   a.cut = a.cut_w = cutout_yx;
   a.flips = a.flips_w = flips;
-  return launch_rrc(a, ffcv::as_stream(stream), p, out);
+  return launch_rrc(c, a, ffcv::as_stream(stream), p, out);
 }
 
 int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, const ffcv_sample *samples,
@@ -2783,12 +2804,13 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   a.out = out;
   a.out_stride = out_stride;
   hipStream_t s = ffcv::as_stream(stream);
-  FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), s));
+  if (int rc = arena_before_k1(c, a, s)) return rc;
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
   dim3 g2((c->max_h + BAND - 1) / BAND, batch);
   hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_FULL, false>), g2, dim3(K2T), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<FULL>");
+  c->arena_zero = true;
   return FFCV_OK;
 }
 
@@ -2802,7 +2824,7 @@ int ffcv_jpeg_coefficients_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *
   a.out = coefs;
   a.out_stride = max_blocks * 64 * 2;
   a.max_blocks = max_blocks;
-  FFCV_HIP_CHECK(hipMemsetAsync(a.arena_top, 0, sizeof(unsigned long long), ffcv::as_stream(stream)));
+  if (int rc2 = arena_before_k1(c, a, ffcv::as_stream(stream))) return rc2;
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_COEF>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0,
                      ffcv::as_stream(stream), a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<COEF>");

@@ -454,6 +454,7 @@ int main(int argc, char **argv) {
       if (steps > rm) rm = steps;
       if (steps > wmax[t / 64]) wmax[t / 64] = steps;
       work += steps;
+      if (getenv("SIM_DUMP")) printf("TASK %d %d %ld\n", rounds, t, steps);
     }
     for (int q = 0; q < (lanes + 63) / 64; q++) { wave_iters += wmax[q]; wmax[q] = 0; }
     memcpy(g, ng, lanes * sizeof(St));

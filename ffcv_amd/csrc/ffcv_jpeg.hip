@@ -171,7 +171,6 @@ struct JShared {
   int nslots;
   int slot_tab[NSLOT];  // class * 4 + id
   uint32_t sinfo[NSLOT];  // see SI_* below
-  uint32_t dinf[10], ainf[10];  // sinfo of each block-in-MCU's DC / AC table
   uint32_t dcpack, acpack, acmask;
   uint32_t scan_off;
   uint32_t dqt_off[4];
@@ -190,10 +189,18 @@ struct JShared {
   uint32_t ds_bytes, cf_bytes, dc_bytes;
   uint32_t dlen;
   int any;
-  // per block-in-MCU descriptor for the write pass: block index of MCU (0,0)
-  // in its component's plane, blocks per MCU row step, hs, and the window
-  // as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
-  int4 pdesc[10][2];
+  // per block-in-MCU (phase) record, read by the decode loops for the phase
+  // that follows the current one: its DC / AC table sinfo, its own successor
+  // (so the loops carry the next phase index instead of computing ph + 1 mod
+  // bpm and its address every step), and the write pass's descriptor: block
+  // index of MCU (0,0) in the component's window, blocks per MCU row step,
+  // hs, and the window as MCU ranges [mx_lo, mx_hi] x [my_lo, my_hi]
+  // (64 bytes: the record address is one shift-add from the phase index)
+  struct __attribute__((aligned(16))) PhaseRec {
+    uint32_t dinf, ainf;
+    int next, pad;
+    int4 pd0, pd1, pad2;
+  } phr[10];
   int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
   int qmax[3];  // max |qmul| of the AC multipliers per component (the IDCT's 32-bit-product test)
   union __attribute__((aligned(16))) {
@@ -451,8 +458,8 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
   br.init(words, st.pos);
   uint32_t pos = st.pos;
   int z = st.z, ph = st.ph;
-  const int bpm = S.bpm;
-  uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
+  uint32_t dinf = S.phr[ph].dinf, ainf = S.phr[ph].ainf;
+  int nph = S.phr[ph].next;
   const int ob = cb, nbuf = cb ^ 1;
   const int onev = use_old ? nev : 0;
   const uint32_t *evo = &S.ev[ob][0][lane];
@@ -463,8 +470,8 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
   bool hit = false;
   while (pos < end_bit && !hit) {
     K1_DIAG(iters++);
-    const int nph = ph + 1 == bpm ? 0 : ph + 1;
-    const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
+    const uint32_t ndinf = S.phr[nph].dinf, nainf = S.phr[nph].ainf;
+    const int nnph = S.phr[nph].next;
     const bool isblk = z == 0;
     const uint32_t key = (pos << 4) | (uint32_t)ph;
     if constexpr (use_old) {
@@ -475,7 +482,12 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
       ocur = adv ? (j < onev ? onext : 0xFFFFFFFFu) : ocur;
     }
     const bool rec = isblk && !hit;
-    evn[(rec && (n & smask) == 0 ? min(n >> sh, NEV) : NEV) * JL] = key;
+    // slot n >> sh at a block start on the slot grid, else the dummy row NEV:
+    // nz is 0 exactly then, and any non-zero nz pushes the index past NEV.
+    // (A hit step may write its key: the splice below copies that same old
+    // event into that slot.)
+    const uint32_t nz = ((uint32_t)n & (uint32_t)smask) | (uint32_t)z;
+    evn[min((n >> sh) + (int)(nz << 8), NEV) * JL] = key;
     n += rec ? 1 : 0;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
     // a pair whose first symbol ends the block decodes that symbol alone
@@ -488,6 +500,7 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
     const bool bend = z >= 64;
     z = bend ? 0 : z;
     ph = bend ? nph : ph;
+    nph = bend ? nnph : nph;
     dinf = bend ? ndinf : dinf;
     ainf = bend ? nainf : ainf;
   }
@@ -565,18 +578,19 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
   int z = st.z, ph = st.ph;
   const int bpm = S.bpm, mcux = S.mcux;
   const uint32_t nblocks = (uint32_t)S.nblocks;
-  uint32_t dinf = S.dinf[ph], ainf = S.ainf[ph];
+  uint32_t dinf = S.phr[ph].dinf, ainf = S.phr[ph].ainf;
+  int nph = S.phr[ph].next;
   int m = (int)(blk / bpm);
   int my = m / mcux, mx = m - my * mcux;
   uint32_t boff;
   bool inwin;
-  locate_block(S.pdesc[ph][0], S.pdesc[ph][1], blk, nblocks, mx, my, boff, inwin);
+  locate_block(S.phr[ph].pd0, S.phr[ph].pd1, blk, nblocks, mx, my, boff, inwin);
   while (pos < end_bit && !(z == 0 && blk >= nblocks)) {
     K1_DIAG(iters++);
     br.begin();
-    const int nph = ph + 1 == bpm ? 0 : ph + 1;
-    const uint32_t ndinf = S.dinf[nph], nainf = S.ainf[nph];
-    const int4 npd0 = S.pdesc[nph][0], npd1 = S.pdesc[nph][1];
+    const uint32_t ndinf = S.phr[nph].dinf, nainf = S.phr[nph].ainf;
+    const int nnph = S.phr[nph].next;
+    const int4 npd0 = S.phr[nph].pd0, npd1 = S.phr[nph].pd1;
     const bool isblk = z == 0;
     const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
     // see make_pair: vs = this step's bits and z advance
@@ -596,6 +610,9 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
 #ifndef K1_TIMING_NOSTORE
     const uint32_t o1 = (boff + (uint32_t)min(z + zinc - 1, 63)) * 2, o2 = (boff + (uint32_t)min(z + zadd - 1, 63)) * 2;
 #ifndef K1_TIMING_NODC
+#ifdef K1_STORE_MASKED
+    if (isblk)
+#endif
     __builtin_amdgcn_raw_buffer_store_b16((short)v, drs, isblk ? blk * 2 : BUF_OOR, 0, 0);
 #endif
 #ifndef K1_TIMING_NOAC
@@ -604,8 +621,15 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     const bool l1 = a1 && stg && p1 < ACS_Z, l2 = a2 && stg && p2 < ACS_Z;
     if (l1) acs16[p1] = (int16_t)v;
     if (l2) acs16[p2] = (int16_t)v2;
+#ifdef K1_STORE_MASKED
+    if (a1 && !l1) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, o1, 0, 0);
+    if (a2 && !l2) __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, o2, 0, 0);
+#elif defined(K1_TIMING_NODIRECT)
+    if (o1 == 0x12345u && o2 == 0x12345u) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, o1, 0, 0);
+#else
     __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, a1 && !l1 ? o1 : BUF_OOR, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, a2 && !l2 ? o2 : BUF_OOR, 0, 0);
+#endif
 #endif
 #else  // timing only (wrong output): the write pass without its stores
     if (v == 0x7fffffff && v2 == 0x7fffffff) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, boff, 0, 0);
@@ -626,6 +650,12 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
         }
       }
       const uint32_t fo = fl ? boff * 2 : BUF_OOR;
+#ifdef K1_FLUSH_MASKED
+      if (fl)
+#endif
+#ifdef K1_TIMING_NOFLUSH
+      if (fo == 0x12345u)
+#endif
 #pragma unroll
       for (int q = 0; q < ACS_BYTES / 16; q++)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, c[q]), crs, fo + 16 * q, 0, 0);
@@ -642,6 +672,7 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     z = bend ? 0 : z;
     blk += bend ? 1 : 0;
     ph = bend ? nph : ph;
+    nph = bend ? nnph : nph;
     mx = bend ? nmx : mx;
     my = bend ? nmy : my;
     dinf = bend ? ndinf : dinf;
@@ -1047,8 +1078,9 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
         nset += bits ? 1u : 0u;
       }
       for (int b = 0; b < nb; b++) {
-        S.dinf[b] = S.sinfo[slot_of(S.dcpack, b)];
-        S.ainf[b] = S.sinfo[slot_of(S.acpack, b)];
+        S.phr[b].dinf = S.sinfo[slot_of(S.dcpack, b)];
+        S.phr[b].ainf = S.sinfo[slot_of(S.acpack, b)];
+        S.phr[b].next = b + 1 == nb ? 0 : b + 1;
       }
       S.scan_off = p + (uint32_t)len;
       have_sos = 1;
@@ -1146,8 +1178,8 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     // base + my * (vs * wbw) + mx * hs (base may be negative: only window
     // blocks are ever addressed, and the sum wraps back in 32 bits)
     const int wbw = S.wx1[c] - S.wx0[c] + 1;
-    S.pdesc[b][0] = make_int4((int)S.coff[c] + (dy - S.wy0[c]) * wbw + (dx - S.wx0[c]), vs * wbw, hs, mxl);
-    S.pdesc[b][1] = make_int4(mxh, myl, myh, 0);
+    S.phr[b].pd0 = make_int4((int)S.coff[c] + (dy - S.wy0[c]) * wbw + (dx - S.wx0[c]), vs * wbw, hs, mxl);
+    S.phr[b].pd1 = make_int4(mxh, myl, myh, 0);
   }
   return FFCV_SAMPLE_OK;
 }

@@ -211,6 +211,8 @@ def main():
     ap.add_argument('--k2flags', type=int, default=0, help='diagnostic: K2 timing-only flags')
     ap.add_argument('--only', type=int, default=0,
                     help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 2 K2)')
+    ap.add_argument('--split', default='',
+                    help='diagnostic: batches per timed launch, comma-separated (must sum to --steps)')
     ap.add_argument('--no-later-epochs', action='store_true',
                     help='skip the later-epoch (entropy index) measurement reported beside the headline')
     ap.add_argument('--entropy-index', action='store_true',
@@ -364,13 +366,18 @@ def main():
             ev[1].record(stream)
         return n
 
+    split = [int(x) for x in args.split.split(',')] if args.split else None
+    if split and (sum(split) != args.steps or max(split) > G):
+        raise SystemExit('bench: --split must sum to --steps with parts <= the group size')
+
     def run_batches(b0, nb, events=None):
         """Batches [b0, b0+nb) in ceil(nb/G) launches of near-equal size (at
         most G batches each), round-robin over the S slot streams."""
-        nl = (nb + G - 1) // G
+        parts = split if split and nb == args.steps else None
+        nl = len(parts) if parts else (nb + G - 1) // G
         done = 0
         for li in range(nl):
-            g = (nb - done) // (nl - li)
+            g = parts[li] if parts else (nb - done) // (nl - li)
             ev = None
             if events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -17,11 +17,11 @@ crop's MCUs) and jpeg_color_resize_kernel (upsample+colour, INTER_AREA,
 cutout, LUT).  The 1.28M-entry dataset is built from U unique encodings
 replicated at distinct HBM addresses.
 
-Launch shape: one decode launch covers ``--group`` consecutive batches (C3:
-8 x 512 = 4,096 images, i.e. 1,024 entropy workgroups = 4 per CU, the
-kernel's full residency), each batch with its own output rows, and
+Launch shape: one decode launch covers up to ``--group`` consecutive batches
+(C3: up to 24 x 512 = 12,288 images, 3,072 entropy workgroups, three times
+the kernel's residency of 4 per CU), each batch with its own output rows, and
 ``--inflight`` launches overlap on their own HIP streams so one launch's
-tail overlaps the next one's start.  Every slot (stream + decoder scratch)
+tail overlaps another's start (launch_sizes).  Every slot (stream + decoder scratch)
 is primed with one untimed launch before the W warmup steps, so no
 first-use cost lands inside the timed region; the timed region is EXACTLY K
 batches, bracketed by barrier + synchronize.
@@ -62,11 +62,12 @@ WORKLOAD = {
 # batches per launch and launches in flight (tools/g_sweep*.sh):
 # a JPEG launch of >= 4,096 images fills K1's residency (4 WGs x 4 images per
 # CU); fewer, larger launches cut the per-launch tails (C3 at 400 steps: 2.62 M/s
-# with 12 batches per launch, 2.74 M/s with 20-32), but a job of K batches
-# keeps at least two launches so one's K1 overlaps the other's K2 (at the
-# driver's 20 steps: 2.48 M/s with 10-12, 2.33 M/s as one launch of 20); the
-# raw kernel has 7,168 workgroups per batch and groups only to cut host
-# submissions
+# with 12 batches per launch, 2.74 M/s with 20-32), but a JPEG job of K
+# batches runs as at least S launches, the first half a share, so one's K1
+# overlaps another's K2 (at the driver's 20 steps: 4 + 8 + 8 gives 2.54-2.57
+# M/s against 2.49-2.51 M/s for 10 + 10 and 2.33 M/s for one launch of 20,
+# launch_sizes); the raw kernel has 7,168 workgroups per batch and groups only
+# to cut host submissions
 GROUP = {'c3': 24, 'c2': 24, 'c5': 4}
 INFLIGHT = {'c3': 3, 'c2': 3, 'c5': 3}
 IMAGENET_MEAN = np.array([0.485, 0.456, 0.406]) * 255
@@ -213,6 +214,8 @@ def main():
                     help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 2 K2)')
     ap.add_argument('--split', default='',
                     help='diagnostic: batches per timed launch, comma-separated (must sum to --steps)')
+    ap.add_argument('--uniform-launches', action='store_true',
+                    help='profiling: ceil(K/G) launches of near-equal size (no half-size first launch)')
     ap.add_argument('--no-later-epochs', action='store_true',
                     help='skip the later-epoch (entropy index) measurement reported beside the headline')
     ap.add_argument('--entropy-index', action='store_true',
@@ -252,7 +255,9 @@ def main():
     mode, side, out, batch, cut, norm, default_n = CONFIGS[args.config]
     if args.batch:  # diagnostic: launch granularity (not the BASELINE config)
         batch = args.batch
-    G = max(1, args.group or min(GROUP[args.config], -(-args.steps // 2)))
+    # slot capacity: GROUP batches whatever K (launch_sizes splits K; at the
+    # driver's 20 steps capacity 24 measured 2.52-2.54 M vs 2.47-2.51 M at 10)
+    G = max(1, args.group or GROUP[args.config])
     S = max(1, args.inflight or INFLIGHT[args.config])
     N = args.dataset_size or default_n
     workers = max(1, min(16, cpu_threads() // max(1, world)))
@@ -370,14 +375,32 @@ def main():
     if split and (sum(split) != args.steps or max(split) > G):
         raise SystemExit('bench: --split must sum to --steps with parts <= the group size')
 
+    def launch_sizes(nb):
+        """Batches per launch for nb batches: at least min(S, nb) launches
+        (every stream busy), at most G batches each; the first launch gets
+        half a share, so its K1 ends early and its K2 fills the others' K1
+        tails (at the driver's 20 steps: 4 + 8 + 8, +2% over 10 + 10 in
+        alternating runs, tools/split_sweep.sh)."""
+        if split and nb == args.steps:
+            return list(split)
+        if args.uniform_launches or mode != 'jpg':  # profiling / one-kernel raw launches: equal sizes
+            nl = (nb + G - 1) // G
+            return [(nb - nb * i // nl) - (nb - nb * (i + 1) // nl) for i in range(nl)][::-1]
+        nl = max((nb + G - 1) // G, min(S, nb))
+        while True:
+            first = max(1, (nb + nl - 1) // (2 * nl - 1)) if nl > 1 else nb
+            rest = [(nb - first) // (nl - 1) + (1 if i < (nb - first) % (nl - 1) else 0)
+                    for i in range(nl - 1)] if nl > 1 else []
+            parts = [first] + rest
+            if max(parts) <= G:
+                return parts
+            nl += 1
+
     def run_batches(b0, nb, events=None):
-        """Batches [b0, b0+nb) in ceil(nb/G) launches of near-equal size (at
-        most G batches each), round-robin over the S slot streams."""
-        parts = split if split and nb == args.steps else None
-        nl = len(parts) if parts else (nb + G - 1) // G
+        """Batches [b0, b0+nb) in the launches launch_sizes(nb) gives,
+        round-robin over the S slot streams."""
         done = 0
-        for li in range(nl):
-            g = parts[li] if parts else (nb - done) // (nl - li)
+        for g in launch_sizes(nb):
             ev = None
             if events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -6,7 +6,8 @@
 # with tracing domains; MI355X_MICROARCH.md rocprofv3 section).
 # Pass 4: SQ instruction / wait counters (8 SQ slots, one pass).
 # Use --steps / --warmup that are multiples of the config's batches per
-# launch so every launch has the same size (tools/pmc_summary.py divides by it).
+# launch and --uniform-launches so every launch has the same size
+# (tools/pmc_summary.py divides by it).
 set -e
 TAG=${1:-r2}; shift || true
 ARGS="${@:---steps 48 --warmup 12 --no-cpu-baseline} --no-host-check --no-later-epochs"

@@ -16,9 +16,9 @@ timeout -k 10 300 python bench.py --entropy-index --no-cpu-baseline > gpurun_out
 FFCV_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 40 --warmup 10 --no-cpu-baseline --no-later-epochs > gpurun_out/${TAG}_bench_2rank.log 2>&1
 for f in bench_driver bench bench_c5 bench_c2 bench_eidx bench_2rank; do tail -1 gpurun_out/${TAG}_$f.log | cut -c1-200; done
 # every profiled launch the same size (C3: 24 batches x 512 per launch, warmup = one launch)
-bash tools/profile.sh ${TAG}_c3 --steps 48 --warmup 24 --no-cpu-baseline
+bash tools/profile.sh ${TAG}_c3 --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c3 12288 gpurun_out/${TAG}_c3_summary.json gpurun_out/traffic_c3.json gpurun_out/sq_c3.json > /dev/null
-bash tools/profile.sh ${TAG}_c5 --config c5 --steps 48 --warmup 12 --no-cpu-baseline
+bash tools/profile.sh ${TAG}_c5 --config c5 --steps 48 --warmup 12 --no-cpu-baseline --uniform-launches
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c5 1024 gpurun_out/${TAG}_c5_summary.json gpurun_out/traffic_c5.json > /dev/null
 if [ -n "$LOADER" ]; then
   timeout -k 10 600 python tools/loader_bench.py --n ${LOADER} > gpurun_out/${TAG}_loader.jsonl 2>&1

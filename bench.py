@@ -211,7 +211,7 @@ def main():
     ap.add_argument('--lib', default=None, help='diagnostic A/B: load this build of libffcv_hip.so')
     ap.add_argument('--k2flags', type=int, default=0, help='diagnostic: K2 timing-only flags')
     ap.add_argument('--only', type=int, default=0,
-                    help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 2 K2)')
+                    help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 1 IDCT, bit 2 K2)')
     ap.add_argument('--split', default='',
                     help='diagnostic: batches per timed launch, comma-separated (must sum to --steps)')
     ap.add_argument('--uniform-launches', action='store_true',
@@ -409,7 +409,7 @@ def main():
             done += g
 
     def check_status(what):
-        if mode != 'jpg':
+        if mode != 'jpg' or args.only:  # --only: timing-only diagnostics (builds may skip the status)
             return
         for i, sl in enumerate(slots):
             if not sl['used']:
@@ -527,7 +527,7 @@ def main():
     hbm = {'bound': 'hbm', 'achieved': round(hbm_achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(hbm_achieved / HBM_PEAK_GBS, 5), 'traffic': None,
            'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note}
-    kernels = (['jpeg_entropy_kernel<0>', 'jpeg_color_resize_kernel<0, true>' if norm else
+    kernels = (['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', 'jpeg_color_resize_kernel<0, true>' if norm else
                 'jpeg_color_resize_kernel<0, false>'] if mode == 'jpg' else ['rrc_raw_kernel<false>'])
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
     # (tools/profile.sh -> tools/pmc_summary.py): bytes per image x images per launch

@@ -121,6 +121,14 @@ struct ImgInfo {
   // taps), computed once per image instead of once per K2 workgroup
   ResizePlan plan;
   int32_t taps;
+  // K1 -> jpeg_idct_kernel: what the DC prediction and the IDCT need
+  uint64_t cf_off, dc_off;  // arena offsets of the window coefficients and the DC differences
+  uint64_t coff[3];         // first window block of each component in the coefficient region
+  uint32_t dc_bytes;
+  int32_t nblocks, bpm, mcux;
+  int32_t hs[3], vs[3], wx0[3], wx1[3], wy0[3], wy1[3], qmax[3];
+  int32_t blk_comp[10], blk_dx[10], blk_dy[10];
+  int16_t qmul[3][64] __attribute__((aligned(16)));
 };
 
 // Linear taps (resize.cpp linear coefficients, LinTap) packed in 8 bytes:
@@ -1756,6 +1764,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     flush((dlen + STREAM_PAD + 3) & ~3u);
   }
   wsync_mem();
+#if defined(K1_STOP) && K1_STOP == 2  // timing only: K1 up to the de-stuffed stream
+  if (dlen != 0x7fffffffu) return;
+#endif
   // one image per wave: its stream base is wave-uniform (scalar registers,
   // so the refill loads use the scalar-base + 32-bit offset form)
   const uint32_t *words = wave_uniform((const uint32_t *)gds);
@@ -1767,49 +1778,88 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid)
                              : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid);
   wsync_mem();
+#if defined(K1_STOP) && K1_STOP == 5  // timing only: K1 up to the write pass
+  if (!any_bad) return;
+#endif
 
   // ------------------------------------------------------------- P6 ----
-  // DC prediction (jdhuff.c last_dc_val): per-component running sum of DC
-  // differences in MCU block order, as a wave scan over block ranges.
+  // DC prediction (jdhuff.c last_dc_val) for the coefficient output (JM_COEF;
+  // the other modes run it in jpeg_idct_kernel): per-component running sum of
+  // DC differences in MCU block order, as a wave scan over block ranges of a
+  // multiple of 8 blocks read as 16-byte buffer loads, DCP_U in flight.
   STAMP(6);
-  {
-    const int nb = S.nblocks;
-    const int per_b = (nb + JL - 1) / JL;
+  if (MODE == JM_COEF) {
+    constexpr int DCP_U = 4;
+    const int nb = S.nblocks, bpm = S.bpm;
+    const int per_b = ((nb + JL - 1) / JL + 7) & ~7;
     const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc(wave_uniform((void *)dcd), 0, (int)wuni(S.dc_bytes), BUF_CFG);
+    auto load8 = [&](int q) -> uint4 {  // blocks b0 + 8q .. b0 + 8q + 7
+      const int b = b0 + 8 * q;
+      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           drs, b < b1 ? (uint32_t)b * 2 : BUF_OOR, 0, 0));
+    };
+    auto diff = [](const uint4 &w, int e) -> int {
+      const uint32_t x = e < 2 ? w.x : e < 4 ? w.y : e < 6 ? w.z : w.w;
+      return (int)(int16_t)(x >> (16 * (e & 1)));
+    };
     int32_t s0 = 0, s1 = 0, s2 = 0;  // (registers: no dynamically indexed arrays)
-    int ph = b0 % S.bpm;
-    for (int b = b0; b < b1; b++) {
-      const int c = S.blk_comp[ph];
-      const int d = dcd[b];
-      s0 += c == 0 ? d : 0;
-      s1 += c == 1 ? d : 0;
-      s2 += c == 2 ? d : 0;
-      if (++ph == S.bpm) ph = 0;
+    int ph = b0 % bpm;
+    for (int q0 = 0; q0 * 8 < per_b; q0 += DCP_U) {
+      uint4 w[DCP_U];
+#pragma unroll
+      for (int u = 0; u < DCP_U; u++) w[u] = load8(q0 + u);
+#pragma unroll
+      for (int u = 0; u < DCP_U; u++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          if (b0 + 8 * (q0 + u) + e < b1) {
+            const int c = S.blk_comp[ph], d = diff(w[u], e);
+            s0 += c == 0 ? d : 0;
+            s1 += c == 1 ? d : 0;
+            s2 += c == 2 ? d : 0;
+            if (++ph == bpm) ph = 0;
+          }
+        }
     }
     int32_t p0 = seg_exscan_i(s0), p1 = seg_exscan_i(s1), p2 = seg_exscan_i(s2);
-    ph = b0 % S.bpm;
-    int m = b0 / S.bpm;
+    ph = b0 % bpm;
+    int m = b0 / bpm;
     int my = m / S.mcux, mx = m - my * S.mcux;
-    for (int b = b0; b < b1; b++) {
-      const int c = S.blk_comp[ph];
-      const int d = dcd[b];
-      p0 += c == 0 ? d : 0;
-      p1 += c == 1 ? d : 0;
-      p2 += c == 2 ? d : 0;
-      const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
-      int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
-      if (bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c])
-        coef[(S.coff[c] + (uint64_t)(by - S.wy0[c]) * (S.wx1[c] - S.wx0[c] + 1) + (bx - S.wx0[c])) * 64] = (int16_t)pv;
-      if (++ph == S.bpm) {
-        ph = 0;
-        if (++mx == S.mcux) {
-          mx = 0;
-          my++;
+    for (int q0 = 0; q0 * 8 < per_b; q0 += DCP_U) {
+      uint4 w[DCP_U];
+#pragma unroll
+      for (int u = 0; u < DCP_U; u++) w[u] = load8(q0 + u);
+#pragma unroll
+      for (int u = 0; u < DCP_U; u++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          if (b0 + 8 * (q0 + u) + e < b1) {
+            const int c = S.blk_comp[ph], d = diff(w[u], e);
+            p0 += c == 0 ? d : 0;
+            p1 += c == 1 ? d : 0;
+            p2 += c == 2 ? d : 0;
+            const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
+            const int bx = mx * S.hs[c] + S.blk_dx[ph], by = my * S.vs[c] + S.blk_dy[ph];
+            if (bx >= S.wx0[c] && bx <= S.wx1[c] && by >= S.wy0[c] && by <= S.wy1[c])
+              coef[(S.coff[c] + (uint64_t)(by - S.wy0[c]) * (S.wx1[c] - S.wx0[c] + 1) + (bx - S.wx0[c])) * 64] =
+                  (int16_t)pv;
+            if (++ph == bpm) {
+              ph = 0;
+              if (++mx == S.mcux) {
+                mx = 0;
+                my++;
+              }
+            }
+          }
         }
-      }
     }
   }
   wsync_mem();
+#if defined(K1_STOP) && K1_STOP == 6  // timing only: K1 up to the DC prediction
+  if (!any_bad) return;
+#endif
 
   if (MODE == JM_COEF) {
     int16_t *o = (int16_t *)a.out + a.out_stride / 2 * k;
@@ -1852,12 +1902,34 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       info->poff[c] = v ? S.poff[c] : 0;
     }
     info->rgb_off = S.rgb_off;
+    info->cf_off = S.cf_off;
+    info->dc_off = S.dc_off;
+    info->dc_bytes = S.dc_bytes;
+    info->nblocks = S.nblocks;
+    info->bpm = S.bpm;
+    info->mcux = S.mcux;
+    for (int c = 0; c < 3; c++) {
+      info->coff[c] = S.coff[c];
+      info->hs[c] = S.hs[c];
+      info->vs[c] = S.vs[c];
+      info->wx0[c] = S.wx0[c];
+      info->wx1[c] = S.wx1[c];
+      info->wy0[c] = S.wy0[c];
+      info->wy1[c] = S.wy1[c];
+      info->qmax[c] = S.qmax[c];
+    }
+    for (int b = 0; b < 10; b++) {
+      info->blk_comp[b] = S.blk_comp[b];
+      info->blk_dx[b] = S.blk_dx[b];
+      info->blk_dy[b] = S.blk_dy[b];
+    }
     info->ri = S.ri;
     info->rj = S.rj;
     info->rh = S.rh;
     info->rw = S.rw;
     a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
   }
+  for (int i = t; i < 3 * 64; i += JL) info->qmul[i >> 6][i & 63] = S.qmul[i >> 6][i & 63];
   if (MODE == JM_RRC) {  // the resize plan and linear taps K2's workgroups share
     const int out_h = a.p.out_h, out_w = a.p.out_w;
     const ResizePlan P = make_plan(S.rw, S.rh, out_w, out_h);
@@ -1875,35 +1947,135 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
   }
 
-  // ------------------------------------------------------------- P8 ----
-  // de-zigzag + dequantise + ifast IDCT (jidctfst.c) of the window's blocks,
-  // one block per lane; each block is zeroed after it is read, which keeps
-  // the coefficient slot all-zero for the next batch.
-  STAMP(8);
+  // (P8, the DC prediction and the IDCT of the window's blocks, is
+  // jpeg_idct_kernel: a launch of its own runs it at VALU throughput instead of
+  // behind this kernel's latency-bound waves, ~25% of K1's time per image)
+  STAMP(9);
+}
+
+// ======================================================================= //
+// K1b: DC prediction + de-zigzag + dequantise + ifast IDCT (jidctfst.c)   //
+// ======================================================================= //
+// One 256-thread workgroup per image.  The DC prediction (jdhuff.c
+// last_dc_val: per-component running sum of the DC differences K1 stored, in
+// MCU block order) is a workgroup scan over block ranges of a multiple of 8
+// blocks (16-byte loads); the absolute DC goes into slot 0 of each window
+// block, then every thread IDCTs window blocks i = t, t + 256, ... into the
+// window planes K2 reads.
+constexpr int K1B_T = 256;
+
+__global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
+  __shared__ ImgInfo L;  // this image's record (per-thread component lookups read LDS)
+  __shared__ int32_t wsum[3][K1B_T / 64];
+  const int k = blockIdx.x, t = threadIdx.x;
+  const ImgInfo &G = a.info[k];
+  if (G.status != FFCV_SAMPLE_OK) return;  // failed (K2 zero-fills) or raw (-1)
+  static_assert(sizeof(ImgInfo) % 4 == 0, "ImgInfo copies as dwords");
+  for (int i = t; i < (int)(sizeof(ImgInfo) / 4); i += K1B_T) ((uint32_t *)&L)[i] = ((const uint32_t *)&G)[i];
+  __syncthreads();
+  int16_t *coef = (int16_t *)(a.arena + L.cf_off);
+  const int nb = L.nblocks, bpm = L.bpm;
   {
-    uint8_t *planes = a.arena;
-    int nb[3];
+    constexpr int U = 2;  // 16-byte loads in flight
+    const int per_b = ((nb + K1B_T - 1) / K1B_T + 7) & ~7;
+    const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(a.arena + L.dc_off), 0, (int)L.dc_bytes, BUF_CFG);
+    auto load8 = [&](int q) -> uint4 {  // blocks b0 + 8q .. b0 + 8q + 7 (inside dc_bytes when b < b1)
+      const int b = b0 + 8 * q;
+      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           drs, b < b1 ? (uint32_t)b * 2 : BUF_OOR, 0, 0));
+    };
+    auto diff = [](const uint4 &w, int e) -> int {
+      const uint32_t x = e < 2 ? w.x : e < 4 ? w.y : e < 6 ? w.z : w.w;
+      return (int)(int16_t)(x >> (16 * (e & 1)));
+    };
+    int32_t s0 = 0, s1 = 0, s2 = 0;
+    int ph = b0 % bpm;
+    for (int q0 = 0; q0 * 8 < per_b; q0 += U) {
+      uint4 w[U];
 #pragma unroll
-    for (int c = 0; c < 3; c++) nb[c] = c < S.ncomp ? (S.wx1[c] - S.wx0[c] + 1) * (S.wy1[c] - S.wy0[c] + 1) : 0;
-    const int ntot = nb[0] + nb[1] + nb[2];
-    for (int i = t; i < ntot; i += JL) {
-      int c = 0, j = i;
-      if (j >= nb[0]) {
-        j -= nb[0];
-        c = 1;
-        if (j >= nb[1]) {
-          j -= nb[1];
-          c = 2;
+      for (int u = 0; u < U; u++) w[u] = load8(q0 + u);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        for (int e = 0; e < 8; e++) {
+          if (b0 + 8 * (q0 + u) + e < b1) {
+            const int c = L.blk_comp[ph], d = diff(w[u], e);
+            s0 += c == 0 ? d : 0;
+            s1 += c == 1 ? d : 0;
+            s2 += c == 2 ? d : 0;
+            if (++ph == bpm) ph = 0;
+          }
         }
-      }
-      const int wbw = S.wx1[c] - S.wx0[c] + 1;
-      const int by = S.wy0[c] + j / wbw, bx = S.wx0[c] + j % wbw;
-      const int stride = wbw * 8;
-      idct_block(coef + (S.coff[c] + (uint64_t)j) * 64, S.qmul[c], S.qmax[c],
-                 planes + S.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
+    }
+    // workgroup exclusive scan of (s0, s1, s2)
+    const int wv = t >> 6;
+    int32_t p0 = wave_exscan_i(s0), p1 = wave_exscan_i(s1), p2 = wave_exscan_i(s2);
+    if ((t & 63) == 63) {
+      wsum[0][wv] = p0 + s0;
+      wsum[1][wv] = p1 + s1;
+      wsum[2][wv] = p2 + s2;
+    }
+    __syncthreads();
+    for (int w = 0; w < wv; w++) {
+      p0 += wsum[0][w];
+      p1 += wsum[1][w];
+      p2 += wsum[2][w];
+    }
+    ph = b0 % bpm;
+    const int m = b0 / bpm;
+    int my = m / L.mcux, mx = m - my * L.mcux;
+    for (int q0 = 0; q0 * 8 < per_b; q0 += U) {
+      uint4 w[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) w[u] = load8(q0 + u);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        for (int e = 0; e < 8; e++) {
+          if (b0 + 8 * (q0 + u) + e < b1) {
+            const int c = L.blk_comp[ph], d = diff(w[u], e);
+            p0 += c == 0 ? d : 0;
+            p1 += c == 1 ? d : 0;
+            p2 += c == 2 ? d : 0;
+            const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
+            const int bx = mx * L.hs[c] + L.blk_dx[ph], by = my * L.vs[c] + L.blk_dy[ph];
+            if (bx >= L.wx0[c] && bx <= L.wx1[c] && by >= L.wy0[c] && by <= L.wy1[c])
+              coef[(L.coff[c] + (uint64_t)(by - L.wy0[c]) * (L.wx1[c] - L.wx0[c] + 1) + (bx - L.wx0[c])) * 64] =
+                  (int16_t)pv;
+            if (++ph == bpm) {
+              ph = 0;
+              if (++mx == L.mcux) {
+                mx = 0;
+                my++;
+              }
+            }
+          }
+        }
     }
   }
-  STAMP(9);
+  __threadfence_block();  // the DC slots written above are read by other threads below
+  __syncthreads();
+  uint8_t *planes = a.arena;
+  int nbw[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) nbw[c] = c < L.ncomp ? (L.wx1[c] - L.wx0[c] + 1) * (L.wy1[c] - L.wy0[c] + 1) : 0;
+  const int ntot = nbw[0] + nbw[1] + nbw[2];
+  for (int i = t; i < ntot; i += K1B_T) {
+    int c = 0, j = i;
+    if (j >= nbw[0]) {
+      j -= nbw[0];
+      c = 1;
+      if (j >= nbw[1]) {
+        j -= nbw[1];
+        c = 2;
+      }
+    }
+    const int wbw = L.wx1[c] - L.wx0[c] + 1;
+    const int by = L.wy0[c] + j / wbw, bx = L.wx0[c] + j % wbw;
+    const int stride = wbw * 8;
+    idct_block(coef + (L.coff[c] + (uint64_t)j) * 64, L.qmul[c], L.qmax[c],
+               planes + L.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
+  }
 }
 
 // ======================================================================= //
@@ -2640,12 +2812,17 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
       (e = hipMemset(c->arena_top, 0, 2 * sizeof(unsigned long long))) != hipSuccess ||
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->taps, sizeof(uint2) * K2_TAPS * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess) {
+      (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess ||
+      // the memset above runs on the null stream, which the caller's
+      // non-blocking streams do not wait for: finish it here (a first launch
+      // on another stream read a stale counter left in reused memory and
+      // failed every image TOO_LARGE)
+      (e = hipStreamSynchronize(nullptr)) != hipSuccess) {
     int rc = ffcv::check_hip(e, "ffcv_jpeg_create: hipMalloc");
     free_ctx(c);
     return rc;
   }
-  c->arena_zero = true;
+  c->arena_zero = false;  // the first launch also zeroes the counter, on its own stream
   *out = c;
   return FFCV_OK;
 }
@@ -2664,8 +2841,8 @@ int ffcv_jpeg_set_debug(ffcv_jpeg_ctx *c, uint64_t *dbg) {
 }
 
 // Diagnostic hook (not in the public header): which kernels a decode launch
-// runs (bit 0 = K1, bit 2 = K2; timing of one kernel re-run on the previous
-// launch's scratch) and K2 timing-only flags.  Set once per context, never
+// runs (bit 0 = K1, bit 1 = the IDCT kernel, bit 2 = K2; timing of one kernel
+// re-run on the previous launch's scratch) and K2 timing-only flags.  Set once per context, never
 // read from the environment on the launch path.
 int ffcv_jpeg_set_diag(ffcv_jpeg_ctx *c, int only, int k2flags) {
   if (!c) return FFCV_EINVAL;
@@ -2764,6 +2941,10 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
                        s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
+  if (only & 2) {
+    hipLaunchKernelGGL(jpeg_idct_kernel, dim3(batch), dim3(K1B_T), 0, s, a);
+    FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
+  }
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (!(only & 4)) {
   } else if (fp16)
@@ -2839,6 +3020,8 @@ int ffcv_jpeg_decode_batch(ffcv_jpeg_ctx *c, void *stream, const uint8_t *base, 
   if (int rc = arena_before_k1(c, a, s)) return rc;
   hipLaunchKernelGGL((jpeg_entropy_kernel<JM_FULL>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<FULL>");
+  hipLaunchKernelGGL(jpeg_idct_kernel, dim3(batch), dim3(K1B_T), 0, s, a);
+  FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
   dim3 g2((c->max_h + BAND - 1) / BAND, batch);
   hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_FULL, false>), g2, dim3(K2T), 0, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<FULL>");

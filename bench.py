@@ -195,7 +195,8 @@ def main():
     ap.add_argument('--steps', type=int, default=400)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='c3', choices=list(CONFIGS))
-    ap.add_argument('--unique', type=int, default=4096)
+    ap.add_argument('--unique', type=int, default=16384,
+                    help='unique synthetic encodings replicated over the dataset (generated once per box, /tmp cache)')
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=10.0)

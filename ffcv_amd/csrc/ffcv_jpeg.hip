@@ -64,12 +64,16 @@
 #define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
 #define FB_AC 11        // first-level bits, the scan's first AC table (luma)
 #define FB_AC2 10       // first-level bits, further AC tables (chroma)
+#ifndef FB_DC
 #define FB_DC 8         // first-level bits, DC tables
+#endif
 // first-level LUT words shared by the slots (+ two zero words): one table of
 // each AC size and two DC tables, the 4:2:0 / 4:2:2 / 4:4:4 norm
 #define LUT_POOL ((1 << FB_AC) + (1 << FB_AC2) + 2 * (1 << FB_DC) + 2)
 #define SUBB 5          // second-level bits
+#ifndef NSUB
 #define NSUB 8          // second-level tables per slot
+#endif
 #define NSLOT 6         // Huffman tables a scan can reference (3 DC + 3 AC)
 #define NLUTSLOT 4      // slots that can get a first-level LUT from the pool
 #define NTAB 8
@@ -209,7 +213,6 @@ struct JShared {
     int next, pad;
     int4 pd0, pd1, pad2;
   } phr[10];
-  int16_t qmul[3][64] __attribute__((aligned(16)));  // ifast dequantisation multipliers (natural order)
   int qmax[3];  // max |qmul| of the AC multipliers per component (the IDCT's 32-bit-product test)
   union __attribute__((aligned(16))) {
     uint8_t hdr[HDR_BYTES];       // P0-P1: the first header bytes
@@ -1634,7 +1637,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     int qv = S.dqt_prec[tq] ? ((HB(q + 2 * zz) << 8) | HB(q + 2 * zz + 1)) : HB(q + zz);
     int n = c_natural[zz];
     const int16_t qmv = (int16_t)(((int64_t)qv * c_aanscales[n] + (1 << 11)) >> 12);
-    S.qmul[c][n] = qmv;
+    info->qmul[c][n] = qmv;  // read by jpeg_idct_kernel only
     if (n != 0) atomicMax(&S.qmax[c], qmv < 0 ? -(int)qmv : (int)qmv);
   }
   wsync_lds();  // header bytes are dead from here (P2 stages into the same LDS)
@@ -1929,7 +1932,6 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     info->rw = S.rw;
     a.status[k] = any_bad ? FFCV_SAMPLE_CORRUPT : FFCV_SAMPLE_OK;
   }
-  for (int i = t; i < 3 * 64; i += JL) info->qmul[i >> 6][i & 63] = S.qmul[i >> 6][i & 63];
   if (MODE == JM_RRC) {  // the resize plan and linear taps K2's workgroups share
     const int out_h = a.p.out_h, out_w = a.p.out_w;
     const ResizePlan P = make_plan(S.rw, S.rh, out_w, out_h);

@@ -251,8 +251,10 @@ int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *ctx, void *stream, const uint8_t *base,
  * runs the self-synchronising Huffman sync and publishes the converged start
  * state of each lane range; a later decode of the same sample (the next
  * epoch) reads it and skips the sync rounds.  Output is bit-identical either
- * way.  NULL detaches.  Records are published with agent-scope release /
- * acquire, so launches on other streams may read them concurrently. */
+ * way.  NULL detaches.  Records are written and read with plain memory
+ * operations and carry a 64-bit hash of their words, so a launch on another
+ * stream that reads a record while it is being published sees a torn record
+ * fail the hash and decodes that sample in full. */
 int ffcv_jpeg_set_entropy_index(ffcv_jpeg_ctx *ctx, uint32_t *index,
                                 uint64_t n_samples);
 

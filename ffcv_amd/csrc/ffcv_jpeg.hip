@@ -1978,7 +1978,6 @@ __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
   int16_t *coef = (int16_t *)(a.arena + L.cf_off);
   const int nb = L.nblocks, bpm = L.bpm;
   {
-    constexpr int U = 2;  // 16-byte loads in flight
     const int per_b = ((nb + K1B_T - 1) / K1B_T + 7) & ~7;
     const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
     const __amdgpu_buffer_rsrc_t drs =
@@ -1994,15 +1993,14 @@ __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
     };
     int32_t s0 = 0, s1 = 0, s2 = 0;
     int ph = b0 % bpm;
-    for (int q0 = 0; q0 * 8 < per_b; q0 += U) {
-      uint4 w[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) w[u] = load8(q0 + u);
-#pragma unroll
-      for (int u = 0; u < U; u++)
+    // the first 8 blocks (all of a thread's blocks up to 2,048 per image) stay
+    // in registers for the second pass
+    const uint4 w0 = load8(0);
+    for (int q = 0; q * 8 < per_b; q++) {
+      const uint4 w = q == 0 ? w0 : load8(q);
         for (int e = 0; e < 8; e++) {
-          if (b0 + 8 * (q0 + u) + e < b1) {
-            const int c = L.blk_comp[ph], d = diff(w[u], e);
+          if (b0 + 8 * q + e < b1) {
+            const int c = L.blk_comp[ph], d = diff(w, e);
             s0 += c == 0 ? d : 0;
             s1 += c == 1 ? d : 0;
             s2 += c == 2 ? d : 0;
@@ -2027,15 +2025,11 @@ __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
     ph = b0 % bpm;
     const int m = b0 / bpm;
     int my = m / L.mcux, mx = m - my * L.mcux;
-    for (int q0 = 0; q0 * 8 < per_b; q0 += U) {
-      uint4 w[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) w[u] = load8(q0 + u);
-#pragma unroll
-      for (int u = 0; u < U; u++)
+    for (int q = 0; q * 8 < per_b; q++) {
+      const uint4 w = q == 0 ? w0 : load8(q);
         for (int e = 0; e < 8; e++) {
-          if (b0 + 8 * (q0 + u) + e < b1) {
-            const int c = L.blk_comp[ph], d = diff(w[u], e);
+          if (b0 + 8 * q + e < b1) {
+            const int c = L.blk_comp[ph], d = diff(w, e);
             p0 += c == 0 ? d : 0;
             p1 += c == 1 ? d : 0;
             p2 += c == 2 ? d : 0;

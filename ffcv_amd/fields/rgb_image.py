@@ -115,15 +115,38 @@ instead."""
             mem_read = self.memory_read
 
             def decode_host(batch_indices, destination, metadata, storage_state):
-                for dst_ix, source_ix in enumerate(batch_indices):
-                    field = metadata[source_ix]
+                # rgb_image.py:123-136 per sample; the raw samples of the batch go
+                # through one native gather (ffcv_host_gather) instead of a
+                # Python-level read + my_memcpy each (C1: 83 k -> see DESIGN s8)
+                B = len(batch_indices)
+                fields = metadata[np.asarray(batch_indices, dtype=np.int64)]
+                raw = fields['mode'] != IMAGE_MODES['jpg']
+                mstate = getattr(storage_state, 'host_state', storage_state)  # BatchContext or the tuple
+                if raw.any() and isinstance(mstate, tuple) and len(mstate) in (3, 4) \
+                        and isinstance(destination, np.ndarray) and destination.flags['C_CONTIGUOUS']:
+                    from ..memory_managers.process_cache import host_source
+                    ptrs = fields['data_ptr'][raw].astype(np.uint64)
+                    all_ptrs, all_sizes = mstate[1], mstate[2]
+                    sizes = all_sizes[np.searchsorted(all_ptrs, ptrs)].astype(np.uint64)
+                    row = destination[0].nbytes
+                    sizes = np.minimum(sizes, np.uint64(row))
+                    src, src_off = host_source(mstate, ptrs)
+                    dst_off = np.nonzero(raw)[0].astype(np.uint64) * np.uint64(row)
+                    # a thread per 4 MB (the native gather spawns its threads per call)
+                    nth = int(min(8, max(1, int(sizes.sum()) >> 22)))
+                    L.host_gather(src, src_off, sizes, dst_off, destination, nthreads=nth)
+                    todo = np.nonzero(~raw)[0]
+                else:
+                    todo = range(B)
+                for dst_ix in todo:
+                    field = fields[dst_ix]
                     image_data = mem_read(field['data_ptr'], storage_state)
                     if field['mode'] == IMAGE_MODES['jpg']:
                         _host_imdecode(L, image_data, destination[dst_ix], int(field['height']),
                                        int(field['width']))
                     else:
                         L.memcpy(image_data, destination[dst_ix])
-                return destination[:len(batch_indices)]
+                return destination[:B]
             return decode_host
 
         f_ix = self._field_index

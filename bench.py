@@ -67,8 +67,9 @@ WORKLOAD = {
 # overlaps another's K2 (at the driver's 20 steps: 4 + 8 + 8 gives 2.54-2.57
 # M/s against 2.49-2.51 M/s for 10 + 10 and 2.33 M/s for one launch of 20,
 # launch_sizes); the raw kernel has 7,168 workgroups per batch and groups only
-# to cut host submissions
-GROUP = {'c3': 24, 'c2': 24, 'c5': 4}
+# to cut host submissions and per-launch tails (C5 at 20 steps: 2.50-2.59 M/s
+# with 10 batches per launch vs 2.41-2.51 M/s with 4; 400 steps equal, 2.87 M/s)
+GROUP = {'c3': 24, 'c2': 24, 'c5': 10}
 INFLIGHT = {'c3': 3, 'c2': 3, 'c5': 3}
 IMAGENET_MEAN = np.array([0.485, 0.456, 0.406]) * 255
 IMAGENET_STD = np.array([0.229, 0.224, 0.225]) * 255

@@ -18,7 +18,7 @@ for f in bench_driver bench bench_c5 bench_c2 bench_eidx bench_2rank; do tail -1
 # every profiled launch the same size (C3: 24 batches x 512 per launch, warmup = one launch)
 bash tools/profile.sh ${TAG}_c3 --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c3 12288 gpurun_out/${TAG}_c3_summary.json gpurun_out/traffic_c3.json gpurun_out/sq_c3.json > /dev/null
-bash tools/profile.sh ${TAG}_c5 --config c5 --steps 48 --warmup 12 --no-cpu-baseline --uniform-launches
+bash tools/profile.sh ${TAG}_c5 --config c5 --steps 48 --warmup 12 --no-cpu-baseline --uniform-launches --group 4
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c5 1024 gpurun_out/${TAG}_c5_summary.json gpurun_out/traffic_c5.json > /dev/null
 if [ -n "$LOADER" ]; then
   timeout -k 10 600 python tools/loader_bench.py --n ${LOADER} > gpurun_out/${TAG}_loader.jsonl 2>&1

@@ -132,6 +132,12 @@ struct ImgInfo {
   int32_t nblocks, bpm, mcux;
   int32_t hs[3], vs[3], wx0[3], wx1[3], wy0[3], wy1[3], qmax[3];
   int32_t blk_comp[10], blk_dx[10], blk_dy[10];
+  // DC prediction (RRC / FULL): slot 0 of a window block holds the running sum,
+  // per component, of the DC differences its decoding lane had read up to and
+  // including it; the absolute DC adds that lane's offset (the sums of the
+  // lanes before it).  lane_blk0[l]: first block lane l started (non-decreasing)
+  uint32_t lane_blk0[64];
+  int32_t lane_off[3][64];
   int16_t qmul[3][64] __attribute__((aligned(16)));
 };
 
@@ -575,7 +581,7 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 template <class TB>
 FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32_t words_bytes, DecState st,
                           uint32_t end_bit, uint32_t blk, gshort_t *coef, uint32_t coef_bytes, gshort_t *dcd,
-                          uint32_t dcd_bytes, uint32_t &iters) {
+                          uint32_t dcd_bytes, uint32_t &iters, bool dc_diffs, int &rs0, int &rs1, int &rs2) {
   uint4 *acs = S.acs[threadIdx.x % JL];
   int16_t *acs16 = (int16_t *)acs;
 #pragma unroll
@@ -596,6 +602,8 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
   uint32_t boff;
   bool inwin;
   locate_block(S.phr[ph].pd0, S.phr[ph].pd1, blk, nblocks, mx, my, boff, inwin);
+  int cc = S.phr[ph].pd1.w;  // component of the block in progress
+  int r0 = 0, r1 = 0, r2 = 0;  // running DC sums of the blocks this lane started
   while (pos < end_bit && !(z == 0 && blk >= nblocks)) {
     K1_DIAG(iters++);
     br.begin();
@@ -620,12 +628,16 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     // second AC coefficient, each out of range when the lane has none
 #ifndef K1_TIMING_NOSTORE
     const uint32_t o1 = (boff + (uint32_t)min(z + zinc - 1, 63)) * 2, o2 = (boff + (uint32_t)min(z + zadd - 1, 63)) * 2;
-#ifndef K1_TIMING_NODC
-#ifdef K1_STORE_MASKED
-    if (isblk)
-#endif
-    __builtin_amdgcn_raw_buffer_store_b16((short)v, drs, isblk ? blk * 2 : BUF_OOR, 0, 0);
-#endif
+    {  // DC: the difference itself (coefficient output) or this lane's running sum
+      const int rsum = (cc == 0 ? r0 : (cc == 1 ? r1 : r2)) + v;
+      r0 = isblk && cc == 0 ? rsum : r0;
+      r1 = isblk && cc == 1 ? rsum : r1;
+      r2 = isblk && cc == 2 ? rsum : r2;
+      if (dc_diffs)
+        __builtin_amdgcn_raw_buffer_store_b16((short)v, drs, isblk ? blk * 2 : BUF_OOR, 0, 0);
+      else if (isblk && inwin)
+        acs16[0] = (int16_t)rsum;  // a DC step starts the block: this lane stages it
+    }
 #ifndef K1_TIMING_NOAC
     const int p1 = min(z + zinc - 1, 63), p2 = min(z + zadd - 1, 63);
     const bool a1 = !isblk && size && inwin, a2 = size2 && inwin;
@@ -690,7 +702,11 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     ainf = bend ? nainf : ainf;
     boff = bend ? nboff : boff;
     inwin = bend ? ninwin : inwin;
+    cc = bend ? npd1.w : cc;
   }
+  rs0 = r0;
+  rs1 = r1;
+  rs2 = r2;
 #ifndef K1_TIMING_NOAC
   if (stg && z > 0 && inwin) {  // stopped inside a staged block: its positions below z are this lane's
     for (int q = 0; q < ACS_Z; q++) {
@@ -837,11 +853,13 @@ FFCV_DEV void idct_ifast_block(int d[64], uint8_t *out, int stride) {
 typedef int16_t s16x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
-FFCV_DEV void idct_block(const int16_t *cp, const int16_t *qm, int qmax, uint8_t *out, int stride) {
+// dc_add: added to the DC coefficient (slot 0) before dequantisation
+FFCV_DEV void idct_block(const int16_t *cp, const int16_t *qm, int qmax, uint8_t *out, int stride, int dc_add) {
   int16_t zz[64];
   int d[64];
 #pragma unroll
   for (int p8 = 0; p8 < 8; p8++) *(uint4 *)(zz + p8 * 8) = ((const uint4 *)cp)[p8];
+  zz[0] = (int16_t)(zz[0] + dc_add);
   // max |AC coefficient| on packed halves (|-32768| reads as 32768
   // unsigned); max(|DC| * |qmul[0]|, max|AC| * max|AC qmul|) bounds every
   // dequantised input (the DC term is the large one: a bright block's DC
@@ -1190,7 +1208,7 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     // blocks are ever addressed, and the sum wraps back in 32 bits)
     const int wbw = S.wx1[c] - S.wx0[c] + 1;
     S.phr[b].pd0 = make_int4((int)S.coff[c] + (dy - S.wy0[c]) * wbw + (dx - S.wx0[c]), vs * wbw, hs, mxl);
-    S.phr[b].pd1 = make_int4(mxh, myl, myh, 0);
+    S.phr[b].pd1 = make_int4(mxh, myl, myh, c);  // .w: the phase's component (write pass DC sums)
   }
   return FFCV_SAMPLE_OK;
 }
@@ -1333,7 +1351,19 @@ FFCV_DEV void zero_window_coefs(const JShared &S, int16_t *coef, int t) {
 
 template <class TB>
 FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, int sg, const uint32_t *words,
-                             uint32_t total_bits, int16_t *coef, int16_t *dcd, uint64_t sample_id) {
+                             uint32_t total_bits, int16_t *coef, int16_t *dcd, uint64_t sample_id, bool dc_diffs) {
+  int rs0 = 0, rs1 = 0, rs2 = 0;
+  uint32_t start_blk = 0;  // first block this lane starts
+  // each lane's DC offsets and start block for jpeg_idct_kernel (non-coefficient modes)
+  auto publish_dc = [&]() {
+    if (dc_diffs) return;
+    const int o0 = seg_exscan_i(rs0), o1 = seg_exscan_i(rs1), o2 = seg_exscan_i(rs2);
+    ImgInfo *info = a.info + k;
+    info->lane_blk0[t] = start_blk;
+    info->lane_off[0][t] = o0;
+    info->lane_off[1][t] = o1;
+    info->lane_off[2][t] = o2;
+  };
   uint32_t nthr = (total_bits + 191) / 192;
   nthr = max(1u, min(nthr, (uint32_t)JL));
   const uint32_t cbits = (total_bits + nthr - 1) / nthr;
@@ -1364,11 +1394,16 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
         g.z = t ? (int)(w1 & 0xff) : 0;
         g.ph = t ? (int)((w1 >> 8) & 0xff) : 0;
         const uint32_t cur = t ? w2 : 0u;
+        start_blk = g.z == 0 ? cur : cur + 1;
         uint32_t it_lane2 = 0;
         if (g.pos < my_end)
           write_range(S, T, words, wuni(S.ds_bytes), g, my_end, cur, wave_uniform((gshort_t *)coef),
-                      wuni(S.cf_bytes), wave_uniform((gshort_t *)dcd), wuni(S.dc_bytes), it_lane2);
+                      wuni(S.cf_bytes), wave_uniform((gshort_t *)dcd), wuni(S.dc_bytes), it_lane2, dc_diffs, rs0,
+                      rs1, rs2);
+      } else {
+        start_blk = (uint32_t)S.nblocks;
       }
+      publish_dc();
       return false;
     }
   }
@@ -1444,12 +1479,15 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   STAMP(5);
   zero_window_coefs(S, coef, t);
   uint32_t it_lane2 = 0;
+  start_blk = blk_base;
   if (active && g.pos < my_end) {
     int64_t cur = g.z == 0 ? (int64_t)blk_base : (int64_t)blk_base - 1;
     if (cur >= 0)
       write_range(S, T, words, wuni(S.ds_bytes), g, my_end, (uint32_t)cur, wave_uniform((gshort_t *)coef),
-                  wuni(S.cf_bytes), wave_uniform((gshort_t *)dcd), wuni(S.dc_bytes), it_lane2);
+                  wuni(S.cf_bytes), wave_uniform((gshort_t *)dcd), wuni(S.dc_bytes), it_lane2, dc_diffs, rs0, rs1,
+                  rs2);
   }
+  publish_dc();
   if (a.dbg) {
     const uint32_t wmax = __reduce_max_sync(~0ull, it_lane2);
     if (t == 0) a.dbg[(uint64_t)k * 16 + 15] = (uint64_t)wmax;
@@ -1778,8 +1816,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 
   int16_t *dcd = (int16_t *)(a.arena + (((uint64_t)wuni((uint32_t)(S.dc_off >> 32)) << 32) | wuni((uint32_t)S.dc_off)));
   const uint64_t sid = a.ids && a.eidx ? a.ids[k] : ~0ull;
-  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid)
-                             : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid);
+  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF)
+                             : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF);
   wsync_mem();
 #if defined(K1_STOP) && K1_STOP == 5  // timing only: K1 up to the write pass
   if (!any_bad) return;
@@ -1958,12 +1996,11 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
 // ======================================================================= //
 // K1b: DC prediction + de-zigzag + dequantise + ifast IDCT (jidctfst.c)   //
 // ======================================================================= //
-// One 256-thread workgroup per image.  The DC prediction (jdhuff.c
-// last_dc_val: per-component running sum of the DC differences K1 stored, in
-// MCU block order) is a workgroup scan over block ranges of a multiple of 8
-// blocks (16-byte loads); the absolute DC goes into slot 0 of each window
-// block, then every thread IDCTs window blocks i = t, t + 256, ... into the
-// window planes K2 reads.
+// One 256-thread workgroup per image; every thread IDCTs window blocks
+// i = t, t + 256, ... into the window planes K2 reads.  The DC prediction
+// (jdhuff.c last_dc_val) is done by K1's write pass as running sums per lane:
+// the absolute DC of a block is its slot 0 plus the offset of the lane that
+// started it (a 6-step search over the lanes' start blocks).
 constexpr int K1B_T = 256;
 
 __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
@@ -1976,81 +2013,6 @@ __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
   for (int i = t; i < (int)(sizeof(ImgInfo) / 4); i += K1B_T) ((uint32_t *)&L)[i] = ((const uint32_t *)&G)[i];
   __syncthreads();
   int16_t *coef = (int16_t *)(a.arena + L.cf_off);
-  const int nb = L.nblocks, bpm = L.bpm;
-  {
-    const int per_b = ((nb + K1B_T - 1) / K1B_T + 7) & ~7;
-    const int b0 = min(nb, per_b * t), b1 = min(nb, per_b * (t + 1));
-    const __amdgpu_buffer_rsrc_t drs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(a.arena + L.dc_off), 0, (int)L.dc_bytes, BUF_CFG);
-    auto load8 = [&](int q) -> uint4 {  // blocks b0 + 8q .. b0 + 8q + 7 (inside dc_bytes when b < b1)
-      const int b = b0 + 8 * q;
-      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           drs, b < b1 ? (uint32_t)b * 2 : BUF_OOR, 0, 0));
-    };
-    auto diff = [](const uint4 &w, int e) -> int {
-      const uint32_t x = e < 2 ? w.x : e < 4 ? w.y : e < 6 ? w.z : w.w;
-      return (int)(int16_t)(x >> (16 * (e & 1)));
-    };
-    int32_t s0 = 0, s1 = 0, s2 = 0;
-    int ph = b0 % bpm;
-    // the first 8 blocks (all of a thread's blocks up to 2,048 per image) stay
-    // in registers for the second pass
-    const uint4 w0 = load8(0);
-    for (int q = 0; q * 8 < per_b; q++) {
-      const uint4 w = q == 0 ? w0 : load8(q);
-        for (int e = 0; e < 8; e++) {
-          if (b0 + 8 * q + e < b1) {
-            const int c = L.blk_comp[ph], d = diff(w, e);
-            s0 += c == 0 ? d : 0;
-            s1 += c == 1 ? d : 0;
-            s2 += c == 2 ? d : 0;
-            if (++ph == bpm) ph = 0;
-          }
-        }
-    }
-    // workgroup exclusive scan of (s0, s1, s2)
-    const int wv = t >> 6;
-    int32_t p0 = wave_exscan_i(s0), p1 = wave_exscan_i(s1), p2 = wave_exscan_i(s2);
-    if ((t & 63) == 63) {
-      wsum[0][wv] = p0 + s0;
-      wsum[1][wv] = p1 + s1;
-      wsum[2][wv] = p2 + s2;
-    }
-    __syncthreads();
-    for (int w = 0; w < wv; w++) {
-      p0 += wsum[0][w];
-      p1 += wsum[1][w];
-      p2 += wsum[2][w];
-    }
-    ph = b0 % bpm;
-    const int m = b0 / bpm;
-    int my = m / L.mcux, mx = m - my * L.mcux;
-    for (int q = 0; q * 8 < per_b; q++) {
-      const uint4 w = q == 0 ? w0 : load8(q);
-        for (int e = 0; e < 8; e++) {
-          if (b0 + 8 * q + e < b1) {
-            const int c = L.blk_comp[ph], d = diff(w, e);
-            p0 += c == 0 ? d : 0;
-            p1 += c == 1 ? d : 0;
-            p2 += c == 2 ? d : 0;
-            const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
-            const int bx = mx * L.hs[c] + L.blk_dx[ph], by = my * L.vs[c] + L.blk_dy[ph];
-            if (bx >= L.wx0[c] && bx <= L.wx1[c] && by >= L.wy0[c] && by <= L.wy1[c])
-              coef[(L.coff[c] + (uint64_t)(by - L.wy0[c]) * (L.wx1[c] - L.wx0[c] + 1) + (bx - L.wx0[c])) * 64] =
-                  (int16_t)pv;
-            if (++ph == bpm) {
-              ph = 0;
-              if (++mx == L.mcux) {
-                mx = 0;
-                my++;
-              }
-            }
-          }
-        }
-    }
-  }
-  __threadfence_block();  // the DC slots written above are read by other threads below
-  __syncthreads();
   uint8_t *planes = a.arena;
   int nbw[3];
 #pragma unroll
@@ -2069,8 +2031,20 @@ __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
     const int wbw = L.wx1[c] - L.wx0[c] + 1;
     const int by = L.wy0[c] + j / wbw, bx = L.wx0[c] + j % wbw;
     const int stride = wbw * 8;
+    // block (c, bx, by) in MCU order, then the lane that started it: its
+    // running DC sum in slot 0 plus that lane's offset is the absolute DC
+    const int hs = L.hs[c], vs = L.vs[c];
+    const int mx = bx / hs, my = by / vs, dx = bx - mx * hs, dy = by - my * vs;
+    int ph = 0;
+    for (int q = 0; q < L.bpm; q++)
+      if (L.blk_comp[q] == c && L.blk_dx[q] == dx && L.blk_dy[q] == dy) ph = q;
+    const uint32_t b = (uint32_t)((my * L.mcux + mx) * L.bpm + ph);
+    int lane = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1)
+      if (lane + st < 64 && L.lane_blk0[lane + st] <= b) lane += st;
     idct_block(coef + (L.coff[c] + (uint64_t)j) * 64, L.qmul[c], L.qmax[c],
-               planes + L.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride);
+               planes + L.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride, L.lane_off[c][lane]);
   }
 }
 

@@ -11,11 +11,16 @@ batch of 512 random-order samples through the hot path
     RandomResizedCropRGBImageDecoder((224,224)) -> Cutout(32,(124,116,103))
       -> ToTensor -> ToDevice -> ToTorchImage -> NormalizeImage(imagenet, fp16)
 
-which lowers to two kernels per launch: jpeg_entropy_kernel<RRC> (descriptor
-gather, crop/cutout draws, parse, de-stuff, parallel Huffman, IDCT of the
-crop's MCUs) and jpeg_color_resize_kernel (upsample+colour, INTER_AREA,
-cutout, LUT).  The 1.28M-entry dataset is built from U unique encodings
-replicated at distinct HBM addresses.
+which lowers to three kernels per launch: jpeg_entropy_kernel<RRC> (K1:
+descriptor gather, crop/cutout draws, parse, de-stuff, parallel Huffman
+decode of the crop's coefficients), jpeg_idct_kernel (K1b: DC prediction,
+dequantise + ifast IDCT of the crop's blocks) and jpeg_color_resize_kernel
+(K2: upsample + colour, INTER_AREA, cutout, LUT).  The 1.28M-entry dataset
+is built from U unique encodings replicated at distinct HBM addresses.
+
+After the timed region (outside it) the rows each slot's last timed launch
+wrote are compared bit for bit with the oracle (parity_check); the line's
+`parity` key reports it and the run exits non-zero on any mismatch.
 
 Launch shape: one decode launch covers up to ``--group`` consecutive batches
 (C3: up to 24 x 512 = 12,288 images, 3,072 entropy workgroups, three times
@@ -182,6 +187,64 @@ def cpu_baseline(cfg, tile, offs, sizes, hs, ws, budget_s=10.0):
                       f'{threads} threads, {el:.1f}s wall; 1 core: {d1} images in {el1:.1f}s'}
 
 
+def parity_check(cfg, slots, order, batch, tile, offs, sizes, hs, ws, rows_total, seed=12345):
+    """The headline's own output against the oracle, outside the timed region
+    (the checker role; VERDICT r2 "next" 1).  The rows each slot's last timed
+    launch wrote are still in its output buffer: from every such launch take
+    its first and last 32 rows plus a seeded random sample (rows_total over
+    all launches), redo the draws and the whole per-sample path on the host
+    -- libjpeg-turbo itself (ifast + fancy, = tjDecompress2 TJFLAG_FASTDCT,
+    libffcv.cpp:104-106) when it is present, then the C INTER_AREA / Cutout /
+    LUT restatement (rgb_image.py:185-210, cutout.py:36-47,
+    normalize.py:58-87) -- under the same (seed, epoch, sample id) draws, and
+    compare crops, cutout corners and output bits exactly."""
+    from oracle import oracle as O
+    mode, side, out, _, cut, norm, _ = CONFIGS[cfg]
+    U = len(offs)
+    rng = np.random.default_rng(seed)
+    live = [sl for sl in slots if sl.get('last')]
+    per = max(64, rows_total // max(1, len(live)))
+    lut = O.normalize_lut(IMAGENET_MEAN, IMAGENET_STD) if norm else None
+    decoder = 'libjpeg-turbo' if mode == 'jpg' and O.use_libjpeg_turbo() else ('oracle' if mode == 'jpg' else 'raw')
+    checked = mism = crop_mism = 0
+    launches = []
+    try:
+        for sl in live:
+            b0, nb, epoch = sl['last']
+            n = nb * batch
+            edge = np.r_[np.arange(min(32, n)), np.arange(max(0, n - 32), n)]
+            rest = np.setdiff1d(np.arange(n), edge)
+            pick = rng.choice(rest, size=min(rest.size, max(0, per - edge.size)), replace=False)
+            rows = np.unique(np.r_[edge, pick]).astype(np.int64)
+            ids = order[b0 * batch + rows].astype(np.uint64)
+            u = (ids % U).astype(np.int64)
+            d_rows = __import__('torch').from_numpy(rows).to(sl['out'].device)
+            got = sl['out'].index_select(0, d_rows).cpu().numpy()
+            got_crops = sl['crops'].index_select(0, d_rows).cpu().numpy()
+            crops, cyx = O.draw_batch(ids, hs[u], ws[u], 0, epoch, out_h=out, out_w=out, cutout_size=cut)
+            samples = [(tile[offs[i]:offs[i] + sizes[i]], int(hs[i]), int(ws[i]), 0 if mode == 'jpg' else 1)
+                       for i in u]
+            want = O.rrc_batch(samples, crops, out, out, cutout_yx=cyx, cutout_size=cut, fill=CUTOUT_FILL[cut],
+                               lut=lut, nthreads=cpu_threads())
+            if sl.get('cut') is not None and cut:
+                got_cut = sl['cut'].index_select(0, d_rows).cpu().numpy()
+                crop_mism += int((got_cut != cyx).any(1).sum())
+            crop_mism += int((got_crops != crops).any(1).sum())
+            bad = (got.view(np.uint8).reshape(len(rows), -1) != want.view(np.uint8).reshape(len(rows), -1)).any(1)
+            mism += int(bad.sum())
+            checked += len(rows)
+            launches.append({'rows_in_launch': n, 'checked': len(rows), 'mismatch': int(bad.sum()),
+                             'first_bad_rows': rows[bad][:4].tolist()})
+    finally:
+        if mode == 'jpg':
+            O.use_libjpeg_turbo(False)
+    return {'checked': checked, 'mismatch': mism, 'crop_mismatch': crop_mism, 'oracle_decoder': decoder,
+            'launches': launches,
+            'note': 'rows of the timed launches still in each slot (every launch\'s first and last 32 + a seeded '
+                    'sample) vs the oracle under the same (seed, epoch, id) draws; bit-exact (fp16 bits) '
+                    'required, checked after the timed region'}
+
+
 def load_profile(name):
     p = os.path.join(ROOT, 'profiles', name)
     if os.path.exists(p):
@@ -220,6 +283,11 @@ def main():
                     help='profiling: ceil(K/G) launches of near-equal size (no half-size first launch)')
     ap.add_argument('--no-later-epochs', action='store_true',
                     help='skip the later-epoch (entropy index) measurement reported beside the headline')
+    ap.add_argument('--no-kernel-events', action='store_true',
+                    help='do not record HIP events around each kernel of the timed launches (per-kernel roofline)')
+    ap.add_argument('--parity-rows', type=int, default=1536,
+                    help='rows of the timed launches compared bit for bit with the oracle after the timed region '
+                         '(0: skip)')
     ap.add_argument('--entropy-index', action='store_true',
                     help='later-epoch rate: attach an entropy index, fill it with one untimed pass over '
                          'the timed samples (epoch 0), then time epoch 1 (new crops, no sync rounds)')
@@ -354,6 +422,9 @@ def main():
         sl, stream = slots[s], streams[s]
         n = nb * batch
         sl['used'] = n  # rows of the slot's status the last launch wrote
+        sl['last'] = (b0, nb, dp.epoch)  # what those rows hold (the parity check's ids and draws)
+        if 'timed' in sl:
+            sl['timed'].append(n)
         ids = d_order[b0 * batch:(b0 + nb) * batch]
         if ev is not None:
             ev[0].record(stream)
@@ -440,6 +511,13 @@ def main():
         sl['used'] = 0
         if (args.only or args.k2flags) and sl['dec'] is not None:  # diagnostic kernel selection
             sl['dec'].set_diag(only=args.only or 7, k2flags=args.k2flags)
+    # per-kernel HIP events inside the library (ffcv_jpeg_set_timing): each
+    # timed launch records events on its own stream around K1, K1b and K2
+    kernel_events = mode == 'jpg' and not args.no_kernel_events
+    if kernel_events:
+        for sl in slots:
+            sl['dec'].set_timing(len(launch_sizes(args.steps)))
+            sl['timed'] = []
     torch.cuda.synchronize()
     events = []
     if dist:
@@ -456,10 +534,31 @@ def main():
         check_status('the timed steps')
     launch_ms = [a.elapsed_time(b) for (a, b), _ in events]
     launch_imgs = [n for _, n in events]
+    kernel_ms = None  # per kernel: [total ms over the timed launches, images]
+    if kernel_events:
+        kernel_ms = np.zeros(3)
+        kernel_imgs = 0
+        for sl in slots:
+            ms = sl['dec'].timing_read()
+            sl['dec'].set_timing(0)
+            if len(ms) != len(sl['timed']):
+                raise SystemExit('bench: kernel event count does not match the slot\'s timed launches')
+            kernel_ms += ms.sum(0)
+            kernel_imgs += sum(sl['timed'])
+            sl.pop('timed')
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    parity = None
+    if args.parity_rows > 0 and not (args.only or args.k2flags):
+        parity = parity_check(args.config, slots, order, batch, tile, offs, sizes, hs, ws, args.parity_rows)
+        if dist:
+            t = torch.tensor([parity['checked'], parity['mismatch'], parity['crop_mismatch']], dtype=torch.int64,
+                             device=dev if backend == 'nccl' else 'cpu')
+            dist.all_reduce(t)
+            parity.update(checked_all_ranks=int(t[0]), mismatch_all_ranks=int(t[1]),
+                          crop_mismatch_all_ranks=int(t[2]))
 
     # Later epochs (reported beside the headline, never as `value`): the
     # Loader's default entropy index (768 B of HBM per sample) records where
@@ -567,6 +666,69 @@ def main():
                          f'{sq.get("_build")}) x images/s; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 '
                          f'VALU instruction'),
                 'hbm': hbm}
+        if kernel_ms is not None and kernel_imgs:
+            # Per kernel (VERDICT r2 "next" 3): durations from the HIP events
+            # the library records around each kernel of every timed launch
+            # (live, this run; launches overlap on S streams, so a kernel's
+            # duration includes time it shares with the other streams' kernels,
+            # as rocprofv3's kernel trace does), counters from the committed
+            # rocprofv3 passes.  issue = SQ_INSTS_VALU per image / ns per image
+            # against 1.2288 wave-instructions per ns (2 cycles per wave64 VALU
+            # instruction; the VOP3 integer forms this code is made of take ~4,
+            # tools/op_rate, so the issue-bound fraction lies between frac and
+            # frac_vop3).  hbm_frac_alg = SURVEY 8(d)'s whole-path algorithmic
+            # bytes per image over this kernel's time; hbm_frac_counter = its
+            # own FETCH_SIZE + WRITE_SIZE per image over its time.
+            per = {}
+            for i, n in enumerate(kernels):
+                ns_img = kernel_ms[i] * 1e6 / kernel_imgs
+                q = sq[n]
+                e = {'launch_ms_events': round(kernel_ms[i] / n_launch, 4),
+                     'ns_per_image_events': round(ns_img, 2),
+                     'valu_per_image': round(q['valu_per_image'], 1),
+                     'issue_frac': round(q['valu_per_image'] / ns_img / (VALU_PEAK_GIPS / 1e3), 4),
+                     'issue_frac_vop3': round(2 * q['valu_per_image'] / ns_img / (VALU_PEAK_GIPS / 1e3), 4),
+                     'hbm_frac_alg': round(unit_bytes / ns_img / HBM_PEAK_GBS, 4)}
+                if 'avg_ns' in q and 'images' in q:
+                    e['profile_avg_ns'] = round(q['avg_ns'], 1)
+                    e['profile_images_per_launch'] = q['images']
+                    e['issue_frac_profile'] = round(
+                        q['valu_per_image'] * q['images'] / q['avg_ns'] / (VALU_PEAK_GIPS / 1e3), 4)
+                    e['hbm_frac_alg_profile'] = round(unit_bytes * q['images'] / q['avg_ns'] / HBM_PEAK_GBS, 4)
+                if q.get('SQ_WAVE_CYCLES'):
+                    e['wait_frac'] = round(q['SQ_WAIT_ANY'] / q['SQ_WAVE_CYCLES'], 4)
+                    # SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md)
+                    cyc = 4 * q['SQ_WAVE_CYCLES'] / max(1.0, q['SQ_WAVES'])
+                    e['cycles_per_wave'] = round(cyc, 0)
+                    e['us_per_wave_at_2.4GHz'] = round(cyc / 2400.0, 2)
+                    e['waves_per_image'] = round(q['SQ_WAVES'] / q['images'], 2)
+                if pm and n in pm and 'fetch_size_kb' in pm[n]:
+                    b = (pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 / pm[n]['images']
+                    e['hbm_bytes_per_image_counter'] = round(b, 1)
+                    e['fetch_bytes_per_image'] = round(pm[n]['fetch_size_kb'] * 1024.0 / pm[n]['images'], 1)
+                    e['write_bytes_per_image'] = round(pm[n]['write_size_kb'] * 1024.0 / pm[n]['images'], 1)
+                    e['hbm_frac_counter'] = round(b / ns_img / HBM_PEAK_GBS, 4)
+                per[n] = e
+            dom = max(kernels, key=lambda n: per[n]['ns_per_image_events'])
+            d = per[dom]
+            # the line's roofline is the dominant kernel's (the contract's
+            # "roofline of the dominant kernel"); the three-kernel sum stays as `path`
+            path = {k2: roof[k2] for k2 in ('bound', 'achieved', 'peak', 'unit', 'frac', 'valu_per_image', 'note')}
+            roof = {'bound': 'issue', 'achieved': round(d['valu_per_image'] / d['ns_per_image_events'], 2),
+                    'peak': VALU_PEAK_GIPS, 'unit': 'G VALU wave-instr/s', 'frac': d['issue_frac'],
+                    'traffic': (round(d['hbm_bytes_per_image_counter'] * imgs_per_launch, 1)
+                                if 'hbm_bytes_per_image_counter' in d else None),
+                    'dominant_kernel': dom, **launch,
+                    'limiter': (f'{dom}: {d.get("us_per_wave_at_2.4GHz", "?")} us per wave (one image per wave), '
+                                f'{100 * d.get("wait_frac", 0):.0f}% of wave cycles waiting; VALU issue '
+                                f'{d["issue_frac"]:.3f} of the 2-cycle peak ({d["issue_frac_vop3"]:.3f} at the '
+                                f'~4-cycle VOP3 cost); HBM {d["hbm_frac_alg"]:.3f} of 8 TB/s by algorithmic bytes, '
+                                f'{d.get("hbm_frac_counter", 0):.3f} by its own counter bytes'),
+                    'note': ('dominant kernel (largest event time per image): achieved = its SQ_INSTS_VALU per '
+                             'image / its ns per image from HIP events recorded around it on its own stream over '
+                             'the timed launches; traffic = its FETCH_SIZE + WRITE_SIZE per image x images per '
+                             'launch (profiles/traffic_*.json)'),
+                    'per_kernel': per, 'path': path, 'hbm': hbm}
     res = {
         'metric': 'device-resident images/s, JPEG->RRC 224x224 batch 512; HBM GB/s vs peak',
         'value': round(value, 1),
@@ -591,6 +753,8 @@ def main():
         'roofline': roof,
         'cpu_baseline': None,
     }
+    if parity is not None:
+        res['parity'] = parity
     if later is not None:
         res['later_epochs'] = later
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -599,6 +763,10 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
+    if parity is not None and (parity['mismatch'] or parity['crop_mismatch']):
+        print(f'bench: ERROR {parity["mismatch"]} of {parity["checked"]} checked rows differ from the oracle '
+              f'({parity["crop_mismatch"]} draw mismatches)', file=sys.stderr, flush=True)
+        sys.exit(4)
     # a host-bound measurement is not a measurement of the path (VERDICT r1:
     # 1.87 of 2.07 ms per step was submission).  Submission is asynchronous, so
     # it only bounds the region as it approaches the wall time; 25% margin.

@@ -551,7 +551,7 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
 // descriptor (loaded at the top of the step) and selected at a block end.
 FFCV_DEV void locate_block(const int4 pd0, const int4 pd1, uint32_t blk, uint32_t nblocks, int mx, int my,
                            uint32_t &boff, bool &inwin) {
-  // pd0 = {base block, blocks per MCU row, hs, mx_lo}, pd1 = {mx_hi, my_lo, my_hi, -}
+  // pd0 = {base block, blocks per MCU row, hs, mx_lo}, pd1 = {mx_hi, my_lo, my_hi, component}
   inwin = blk < nblocks && mx >= pd0.w && mx <= pd1.x && my >= pd1.y && my <= pd1.z;
   boff = ((uint32_t)pd0.x + __umul24((uint32_t)my, (uint32_t)pd0.y) + __umul24((uint32_t)mx, (uint32_t)pd0.z)) * 64u;
 }
@@ -2005,7 +2005,6 @@ constexpr int K1B_T = 256;
 
 __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
   __shared__ ImgInfo L;  // this image's record (per-thread component lookups read LDS)
-  __shared__ int32_t wsum[3][K1B_T / 64];
   const int k = blockIdx.x, t = threadIdx.x;
   const ImgInfo &G = a.info[k];
   if (G.status != FFCV_SAMPLE_OK) return;  // failed (K2 zero-fills) or raw (-1)
@@ -2039,10 +2038,10 @@ __global__ void __launch_bounds__(K1B_T) jpeg_idct_kernel(JpegArgs a) {
     for (int q = 0; q < L.bpm; q++)
       if (L.blk_comp[q] == c && L.blk_dx[q] == dx && L.blk_dy[q] == dy) ph = q;
     const uint32_t b = (uint32_t)((my * L.mcux + mx) * L.bpm + ph);
-    int lane = 0;
+    int lane = 0;  // K1 wrote lane_blk0 / lane_off for its JL lanes only
 #pragma unroll
-    for (int st = 32; st >= 1; st >>= 1)
-      if (lane + st < 64 && L.lane_blk0[lane + st] <= b) lane += st;
+    for (int st = JL / 2; st >= 1; st >>= 1)
+      if (lane + st < JL && L.lane_blk0[lane + st] <= b) lane += st;
     idct_block(coef + (L.coff[c] + (uint64_t)j) * 64, L.qmul[c], L.qmax[c],
                planes + L.poff[c] + (uint64_t)by * 8 * stride + bx * 8, stride, L.lane_off[c][lane]);
   }
@@ -2736,11 +2735,23 @@ struct ffcv_jpeg_ctx {
   uint64_t gtab_slot;
   uint32_t *eidx;  // entropy index (caller-owned), or NULL
   uint64_t eidx_n;
+  // per-kernel timing (ffcv_jpeg_set_timing): 4 events per launch recorded on
+  // the launch's stream before K1, after K1, after K1b and after K2
+  hipEvent_t *tev;
+  int tev_cap, tev_n;
 };
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+static void free_timing(ffcv_jpeg_ctx *c) {
+  for (int i = 0; i < 4 * c->tev_cap; i++) (void)hipEventDestroy(c->tev[i]);
+  delete[] c->tev;
+  c->tev = nullptr;
+  c->tev_cap = c->tev_n = 0;
+}
+
 static void free_ctx(ffcv_jpeg_ctx *c) {
+  free_timing(c);
   (void)hipFree(c->arena);
   (void)hipFree(c->arena_top);
   (void)hipFree(c->info);
@@ -2818,6 +2829,43 @@ int ffcv_jpeg_set_diag(ffcv_jpeg_ctx *c, int only, int k2flags) {
   if (!c) return FFCV_EINVAL;
   c->diag_only = only ? only : 7;
   c->diag_k2flags = k2flags;
+  return FFCV_OK;
+}
+
+int ffcv_jpeg_set_timing(ffcv_jpeg_ctx *c, int max_launches) {
+  if (!c || max_launches < 0) {
+    ffcv::set_error("ffcv_jpeg_set_timing: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  free_timing(c);
+  if (!max_launches) return FFCV_OK;
+  c->tev = new hipEvent_t[4 * (size_t)max_launches]();
+  for (int i = 0; i < 4 * max_launches; i++) {
+    hipError_t e = hipEventCreate(&c->tev[i]);
+    if (e != hipSuccess) {
+      c->tev_cap = i / 4;  // destroy what was made (whole sets, then the partial one)
+      for (int j = 4 * c->tev_cap; j < i; j++) (void)hipEventDestroy(c->tev[j]);
+      free_timing(c);
+      return ffcv::check_hip(e, "ffcv_jpeg_set_timing: hipEventCreate");
+    }
+  }
+  c->tev_cap = max_launches;
+  c->tev_n = 0;
+  return FFCV_OK;
+}
+
+int ffcv_jpeg_timing_read(ffcv_jpeg_ctx *c, float *ms, int max_launches, int *n_launches) {
+  if (!c || !n_launches || (max_launches && !ms)) {
+    ffcv::set_error("ffcv_jpeg_timing_read: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  const int n = c->tev_n < max_launches ? c->tev_n : max_launches;
+  for (int i = 0; i < n; i++) {
+    FFCV_HIP_CHECK(hipEventSynchronize(c->tev[4 * i + 3]));
+    for (int q = 0; q < 3; q++) FFCV_HIP_CHECK(hipEventElapsedTime(&ms[3 * i + q], c->tev[4 * i + q], c->tev[4 * i + q + 1]));
+  }
+  *n_launches = n;
+  c->tev_n = 0;
   return FFCV_OK;
 }
 
@@ -2907,14 +2955,21 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   const int only = a.diag_only;
   if (only & 1) {
     if (int rc = arena_before_k1(c, a, s)) return rc;
+  }
+  // per-kernel timing: events around each kernel on this stream
+  hipEvent_t *ev = c->tev_n < c->tev_cap ? c->tev + 4 * c->tev_n++ : nullptr;
+  if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[0], s));
+  if (only & 1) {
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), K1_PAD,
                        s, a);
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
+  if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[1], s));
   if (only & 2) {
     hipLaunchKernelGGL(jpeg_idct_kernel, dim3(batch), dim3(K1B_T), 0, s, a);
     FFCV_LAUNCH_CHECK("jpeg_idct_kernel");
   }
+  if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[2], s));
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (!(only & 4)) {
   } else if (fp16)
@@ -2922,6 +2977,7 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   else
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, false>), g2, dim3(K2T), K2_LDS, s, a);
   FFCV_LAUNCH_CHECK("jpeg_color_resize_kernel<RRC>");
+  if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[3], s));
   if (only & 4) c->arena_zero = true;
   return FFCV_OK;
 }

@@ -348,17 +348,10 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
 
 
 class RandomResizedCropRGBImageDecoder(ResizedCropRGBImageDecoder):
-    """Random crop + resize (rgb_image.py:220-242).
-
-    Parameters
-    ----------
-    output_size : Tuple[int]
-        The desired resized resolution of the images
-    scale : Tuple[float]
-        The range of possible ratios (in area) than can randomly sampled
-    ratio : Tuple[float]
-        The range of potential aspect ratios that can be randomly sampled
-    """
+    """Random crop + resize (rgb_image.py:220-242): ``output_size`` is the
+    (height, width) every crop is resized to; a crop's area is a fraction
+    of the image drawn from ``scale`` and its width/height from ``ratio``
+    (log-uniform), torchvision's RandomResizedCrop rule (get_random_crop)."""
     crop_kind = 0
 
     def __init__(self, output_size, scale=(0.08, 1.0), ratio=(0.75, 4 / 3)):

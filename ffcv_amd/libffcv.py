@@ -92,6 +92,8 @@ _SIGS = {
     'ffcv_jpeg_set_diag': (c_int, [c_void_p, c_int, c_int]),
     'ffcv_jpeg_arena_used': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'ffcv_jpeg_set_entropy_index': (c_int, [c_void_p, c_void_p, c_uint64]),
+    'ffcv_jpeg_set_timing': (c_int, [c_void_p, c_int]),
+    'ffcv_jpeg_timing_read': (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     'ffcv_jpeg_rrc_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'ffcv_jpeg_rrc_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
@@ -389,6 +391,21 @@ class JpegDecoder:
         _check(lib().ffcv_jpeg_set_entropy_index(self.handle, _p(index), int(index.shape[0])),
                'ffcv_jpeg_set_entropy_index')
         self._eidx = index  # keep it alive while attached
+
+    def set_timing(self, max_launches):
+        """Record HIP events around each kernel of the next max_launches RRC
+        launches (0: off); timing_read() returns their durations."""
+        self._tcap = int(max_launches)
+        _check(lib().ffcv_jpeg_set_timing(self.handle, self._tcap), 'ffcv_jpeg_set_timing')
+
+    def timing_read(self):
+        """ms[launch, kernel] (kernel 0 entropy, 1 IDCT, 2 colour/resize) of
+        the launches recorded since set_timing / the last read."""
+        cap = getattr(self, '_tcap', 0)
+        ms = np.zeros((max(1, cap), 3), np.float32)
+        n = c_int()
+        _check(lib().ffcv_jpeg_timing_read(self.handle, _p(ms), cap, ctypes.byref(n)), 'ffcv_jpeg_timing_read')
+        return ms[:n.value]
 
     def coefficients(self, base, samples, batch, out, max_blocks, status, stream=None):
         _check(lib().ffcv_jpeg_coefficients_batch(self.handle, _stream(stream), _p(base),

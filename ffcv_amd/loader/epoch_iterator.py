@@ -52,14 +52,24 @@ class DecodeError(RuntimeError):
     pass
 
 
+_HW_QUEUES = None
+
+
 def hw_queues():
-    """Hardware queues HIP gives this process: GPU_MAX_HW_QUEUES as it was
-    when the runtime initialised (ffcv never rewrites it), HIP's default 4
-    when unset."""
-    try:
-        return max(1, int(os.environ.get('GPU_MAX_HW_QUEUES', '4')))
-    except ValueError:
-        return 4
+    """Hardware queues HIP gives this process: GPU_MAX_HW_QUEUES (HIP's
+    default 4 when unset), read ONCE.  HIP reads the variable when its
+    runtime initialises and never again; the first call here comes from an
+    EpochIterator, after the Loader has initialised the device
+    (``torch.cuda.set_device``), so the cached value is the one in force
+    then, and a later change of the environment (which the runtime ignores)
+    does not change the stream count either."""
+    global _HW_QUEUES
+    if _HW_QUEUES is None:
+        try:
+            _HW_QUEUES = max(1, int(os.environ.get('GPU_MAX_HW_QUEUES', '4')))
+        except ValueError:
+            _HW_QUEUES = 4
+    return _HW_QUEUES
 
 
 def max_streams():
@@ -110,7 +120,16 @@ class EpochIterator(threading.Thread):
         self._cv = threading.Condition()
         self._released = [True] * self.n_sets      # set may be (re)filled
         self._release_event = [None] * self.n_sets  # consumer-stream event to wait on
-        self._pending_release = None                # set whose last batch the consumer holds
+        # [set, batches still to hand out before it is released]: the set of a
+        # batch the consumer got is released when it asks for the hold-th
+        # batch after it, so a batch the training loop keeps (logging,
+        # lookahead) stays intact while it takes batches_ahead more, as with
+        # the reference's ring.  Bound: the producer hands out launch m + 2's
+        # batches only after it has re-acquired launch m's set for m + 3, so
+        # the consumer can take (n_sets - 2) * G batches past a set before it
+        # must have released it
+        self._pending_release = []
+        self._hold = max(1, min(loader.batches_ahead + 1, (self.n_sets - 2) * self.G + 1))
         self._status = [None] * self.n_sets
         self._t_pipeline = 0.0
         self.start()
@@ -280,18 +299,24 @@ class EpochIterator(threading.Thread):
 
     # ----------------------------------------------------------- consumer --
     def _release_pending(self):
-        """The consumer is done enqueueing work on the set it held last."""
-        s = self._pending_release
-        if s is None:
+        """One more batch is being handed out: release every set whose hold
+        ran out (the consumer is done enqueueing work on it)."""
+        if not self._pending_release:
             return
-        self._pending_release = None
+        for p in self._pending_release:
+            p[1] -= 1
+        due = [p[0] for p in self._pending_release if p[1] <= 0]
+        if not due:
+            return
+        self._pending_release = [p for p in self._pending_release if p[1] > 0]
         ev = None
         if self.is_cuda:
             ev = ch.cuda.Event()
             ev.record(self.current_stream)
         with self._cv:
-            self._release_event[s] = ev
-            self._released[s] = True
+            for s in due:
+                self._release_event[s] = ev
+                self._released[s] = True
             self._cv.notify_all()
 
     def __next__(self):
@@ -310,7 +335,7 @@ class EpochIterator(threading.Thread):
         if self.is_cuda:
             self.current_stream.wait_stream(self.cuda_streams[s])
         if last:
-            self._pending_release = s
+            self._pending_release.append([s, self._hold])
         if self.error is not None:
             self.close()
             raise self.error

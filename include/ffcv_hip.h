@@ -258,6 +258,17 @@ int ffcv_jpeg_rrc_fused(ffcv_jpeg_ctx *ctx, void *stream, const uint8_t *base,
 int ffcv_jpeg_set_entropy_index(ffcv_jpeg_ctx *ctx, uint32_t *index,
                                 uint64_t n_samples);
 
+/* Measurement (no reference counterpart; bench.py's per-kernel roofline):
+ * with max_launches > 0 the next max_launches RRC launches on this context
+ * record HIP events on their own stream before the entropy kernel, after
+ * it, after the IDCT kernel and after the colour/resize kernel; 0 turns it
+ * off.  ffcv_jpeg_timing_read waits for the recorded launches and writes
+ * ms[3*i + {0,1,2}] = the three kernels' durations of launch i (in launch
+ * order, at most max_launches), then starts a new recording. */
+int ffcv_jpeg_set_timing(ffcv_jpeg_ctx *ctx, int max_launches);
+int ffcv_jpeg_timing_read(ffcv_jpeg_ctx *ctx, float *ms, int max_launches,
+                          int *n_launches);
+
 /* rgb_image.py:123-136 SimpleRGBImageDecoder jpg branch (imdecode into the
  * destination, full image) -> device [B][H][W][3] with out_stride bytes per
  * sample. */

@@ -559,6 +559,24 @@ def main():
             dist.all_reduce(t)
             parity.update(checked_all_ranks=int(t[0]), mismatch_all_ranks=int(t[1]),
                           crop_mismatch_all_ranks=int(t[2]))
+    # Isolated per-kernel durations (after the parity check: this reuses slot
+    # 0): launches of G batches run one at a time on one stream, so each of
+    # K1 / K1b / K2 has the GPU to itself while its events tick -- the kernel's
+    # own rate, where the timed region's overlapped launches share the CUs
+    iso_ms, iso_imgs = None, 0
+    if kernel_events:
+        sl0 = slots[0]
+        sl0['dec'].set_timing(3)
+        for r in range(3):
+            b0 = (r * G) % prime_batches  # the priming batches: prime_batches = S * G
+            ids = d_order[b0 * batch:(b0 + G) * batch]
+            sl0['dec'].rrc_fused(d_data, d_table, ids, dp, sl0['crops'][:cap], sl0['cut'][:cap] if cut else None,
+                                 None, rp, sl0['out'][:cap], sl0['status'][:cap], stream=streams[0])
+            streams[0].synchronize()
+            iso_imgs += cap
+        iso_ms = sl0['dec'].timing_read().sum(0)
+        sl0['dec'].set_timing(0)
+        sl0['last'] = None
 
     # Later epochs (reported beside the headline, never as `value`): the
     # Loader's default entropy index (768 B of HBM per sample) records where
@@ -679,21 +697,27 @@ def main():
             # frac_vop3).  hbm_frac_alg = SURVEY 8(d)'s whole-path algorithmic
             # bytes per image over this kernel's time; hbm_frac_counter = its
             # own FETCH_SIZE + WRITE_SIZE per image over its time.
+            # (ns per image -> VALU wave-instr per ns = G/s against 1228.8 G/s;
+            # bytes per ns = GB/s against 8000 GB/s)
             per = {}
             for i, n in enumerate(kernels):
-                ns_img = kernel_ms[i] * 1e6 / kernel_imgs
                 q = sq[n]
-                e = {'launch_ms_events': round(kernel_ms[i] / n_launch, 4),
-                     'ns_per_image_events': round(ns_img, 2),
+                ns_ov = kernel_ms[i] * 1e6 / kernel_imgs
+                ns_img = iso_ms[i] * 1e6 / iso_imgs if iso_ms is not None else ns_ov
+                e = {'ns_per_image_isolated': round(ns_img, 2),
+                     'launch_ms_isolated': round(ns_img * cap / 1e6, 4),
+                     'isolated_images_per_launch': cap,
                      'valu_per_image': round(q['valu_per_image'], 1),
-                     'issue_frac': round(q['valu_per_image'] / ns_img / (VALU_PEAK_GIPS / 1e3), 4),
-                     'issue_frac_vop3': round(2 * q['valu_per_image'] / ns_img / (VALU_PEAK_GIPS / 1e3), 4),
-                     'hbm_frac_alg': round(unit_bytes / ns_img / HBM_PEAK_GBS, 4)}
+                     'issue_frac': round(q['valu_per_image'] / ns_img / VALU_PEAK_GIPS, 4),
+                     'issue_frac_vop3': round(2 * q['valu_per_image'] / ns_img / VALU_PEAK_GIPS, 4),
+                     'hbm_frac_alg': round(unit_bytes / ns_img / HBM_PEAK_GBS, 4),
+                     'ns_per_image_overlapped': round(ns_ov, 2),
+                     'launch_ms_overlapped': round(kernel_ms[i] / n_launch, 4),
+                     'issue_frac_overlapped': round(q['valu_per_image'] / ns_ov / VALU_PEAK_GIPS, 4)}
                 if 'avg_ns' in q and 'images' in q:
                     e['profile_avg_ns'] = round(q['avg_ns'], 1)
                     e['profile_images_per_launch'] = q['images']
-                    e['issue_frac_profile'] = round(
-                        q['valu_per_image'] * q['images'] / q['avg_ns'] / (VALU_PEAK_GIPS / 1e3), 4)
+                    e['issue_frac_profile'] = round(q['valu_per_image'] * q['images'] / q['avg_ns'] / VALU_PEAK_GIPS, 4)
                     e['hbm_frac_alg_profile'] = round(unit_bytes * q['images'] / q['avg_ns'] / HBM_PEAK_GBS, 4)
                 if q.get('SQ_WAVE_CYCLES'):
                     e['wait_frac'] = round(q['SQ_WAIT_ANY'] / q['SQ_WAVE_CYCLES'], 4)
@@ -709,12 +733,12 @@ def main():
                     e['write_bytes_per_image'] = round(pm[n]['write_size_kb'] * 1024.0 / pm[n]['images'], 1)
                     e['hbm_frac_counter'] = round(b / ns_img / HBM_PEAK_GBS, 4)
                 per[n] = e
-            dom = max(kernels, key=lambda n: per[n]['ns_per_image_events'])
+            dom = max(kernels, key=lambda n: per[n]['ns_per_image_isolated'])
             d = per[dom]
             # the line's roofline is the dominant kernel's (the contract's
             # "roofline of the dominant kernel"); the three-kernel sum stays as `path`
             path = {k2: roof[k2] for k2 in ('bound', 'achieved', 'peak', 'unit', 'frac', 'valu_per_image', 'note')}
-            roof = {'bound': 'issue', 'achieved': round(d['valu_per_image'] / d['ns_per_image_events'], 2),
+            roof = {'bound': 'issue', 'achieved': round(d['valu_per_image'] / d['ns_per_image_isolated'], 2),
                     'peak': VALU_PEAK_GIPS, 'unit': 'G VALU wave-instr/s', 'frac': d['issue_frac'],
                     'traffic': (round(d['hbm_bytes_per_image_counter'] * imgs_per_launch, 1)
                                 if 'hbm_bytes_per_image_counter' in d else None),
@@ -724,10 +748,12 @@ def main():
                                 f'{d["issue_frac"]:.3f} of the 2-cycle peak ({d["issue_frac_vop3"]:.3f} at the '
                                 f'~4-cycle VOP3 cost); HBM {d["hbm_frac_alg"]:.3f} of 8 TB/s by algorithmic bytes, '
                                 f'{d.get("hbm_frac_counter", 0):.3f} by its own counter bytes'),
-                    'note': ('dominant kernel (largest event time per image): achieved = its SQ_INSTS_VALU per '
-                             'image / its ns per image from HIP events recorded around it on its own stream over '
-                             'the timed launches; traffic = its FETCH_SIZE + WRITE_SIZE per image x images per '
-                             'launch (profiles/traffic_*.json)'),
+                    'note': ('dominant kernel (largest isolated time per image): achieved = its SQ_INSTS_VALU per '
+                             'image (profiles/sq_*.json) / its ns per image from HIP events recorded around it on its '
+                             'own stream in 3 launches of G batches run one at a time after the timed region (the '
+                             'kernel alone on the GPU); per_kernel also gives the events of the timed region\'s '
+                             'overlapped launches and the rocprofv3 profile\'s avg_ns; traffic = its FETCH_SIZE + '
+                             'WRITE_SIZE per image x images per launch (profiles/traffic_*.json)'),
                     'per_kernel': per, 'path': path, 'hbm': hbm}
     res = {
         'metric': 'device-resident images/s, JPEG->RRC 224x224 batch 512; HBM GB/s vs peak',

@@ -1477,6 +1477,9 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 
   // ------------------------------------------------------------- P5 ----
   STAMP(5);
+#if defined(K1_STOP) && K1_STOP == 4  // timing only: K1 up to the sync pass (no write pass)
+  if (nthr != 0x7fffffffu) return any_bad;
+#endif
   zero_window_coefs(S, coef, t);
   uint32_t it_lane2 = 0;
   start_blk = blk_base;

@@ -245,6 +245,33 @@ def parity_check(cfg, slots, order, batch, tile, offs, sizes, hs, ws, rows_total
                     'required, checked after the timed region'}
 
 
+def c5_subresult(timeout_s=150):
+    """BASELINE configs[4] (C5, "the HBM-bound roofline point": raw 512x512
+    RGB, RRC 448 + Cutout 64, batch 256) measured beside the headline, never
+    as `value`: this script in a child process with --config c5 (1,024
+    unique raw encodings replicated to the 10,000-sample .beton, 40 timed
+    steps, parity-checked); its line is returned with its own roofline."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', 'c5', '--steps', '40', '--warmup', '10',
+           '--unique', '1024', '--no-cpu-baseline', '--parity-rows', '512']
+    env = dict(os.environ)
+    for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired:
+        return {'error': f'c5 run exceeded {timeout_s}s'}
+    lines = [l for l in r.stdout.strip().splitlines() if l.startswith('{')]
+    if r.returncode != 0 or not lines:
+        return {'error': f'c5 run failed (rc {r.returncode}): {r.stderr.strip()[-400:]}'}
+    d = json.loads(lines[-1])
+    keep = ('metric', 'value', 'unit', 'steps', 'warmup', 'ms_per_step', 'dtype', 'data', 'config', 'roofline',
+            'parity')
+    out = {k: d[k] for k in keep if k in d}
+    out['command'] = ' '.join(['bench.py'] + cmd[2:])
+    return out
+
+
 def load_profile(name):
     p = os.path.join(ROOT, 'profiles', name)
     if os.path.exists(p):
@@ -283,6 +310,8 @@ def main():
                     help='profiling: ceil(K/G) launches of near-equal size (no half-size first launch)')
     ap.add_argument('--no-later-epochs', action='store_true',
                     help='skip the later-epoch (entropy index) measurement reported beside the headline')
+    ap.add_argument('--no-c5', action='store_true',
+                    help='skip the C5 (raw, HBM-bound) sub-result the default C3 run reports beside its value')
     ap.add_argument('--no-kernel-events', action='store_true',
                     help='do not record HIP events around each kernel of the timed launches (per-kernel roofline)')
     ap.add_argument('--parity-rows', type=int, default=1536,
@@ -543,7 +572,7 @@ def main():
             sl['dec'].set_timing(0)
             if len(ms) != len(sl['timed']):
                 raise SystemExit('bench: kernel event count does not match the slot\'s timed launches')
-            kernel_ms += ms.sum(0)
+            kernel_ms += ms.astype(np.float64).sum(0)
             kernel_imgs += sum(sl['timed'])
             sl.pop('timed')
     if dist:
@@ -574,7 +603,7 @@ def main():
                                  None, rp, sl0['out'][:cap], sl0['status'][:cap], stream=streams[0])
             streams[0].synchronize()
             iso_imgs += cap
-        iso_ms = sl0['dec'].timing_read().sum(0)
+        iso_ms = sl0['dec'].timing_read().astype(np.float64).sum(0)
         sl0['dec'].set_timing(0)
         sl0['last'] = None
 
@@ -785,8 +814,10 @@ def main():
         res['later_epochs'] = later
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(args.config, tile, offs, sizes, hs, ws, args.cpu_budget)
+    if rank == 0 and world == 1 and args.config == 'c3' and not args.no_c5 and not (args.only or args.k2flags):
+        res['c5'] = c5_subresult()
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res, default=lambda o: o.item() if hasattr(o, 'item') else str(o)), flush=True)
     if dist:
         dist.destroy_process_group()
     if parity is not None and (parity['mismatch'] or parity['crop_mismatch']):

@@ -86,8 +86,11 @@ struct LdsSrc {
 //   writes one contiguous run of the output row.
 //   Otherwise (area downscale, copy, widths not a multiple of 4): the
 //   per-pixel restatement, over the staged rows when they fit.
+#ifndef RRC_WPE
+#define RRC_WPE 5  // waves per SIMD the raw kernel is compiled for (5 workgroups per CU by LDS)
+#endif
 template <bool FP16>
-__global__ void __launch_bounds__(RRC_THREADS)
+__global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_eu(RRC_WPE)))
     rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
                    const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
                    const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
@@ -179,28 +182,150 @@ __global__ void __launch_bounds__(RRC_THREADS)
   const int nq = out_w >> 2;  // column quads
   if (staged && (out_w & 3) == 0 && nq <= RRC_THREADS && aligned4 &&
       ((P.kind == 3 && P.vec_end == 3 * out_w) || P.kind == 2)) {
+    if (P.kind == 2 && P.scale_x < 2.0 && P.scale_y < 2.0 && (out_w >> 1) <= RRC_THREADS) {
+      // ResizeArea_Invoker for scales in [1, 2): every destination index takes
+      // at most 3 consecutive source indices, so a fixed 3-tap body with zero
+      // weights past `hi` is exact (x + S * 0.f == x for the non-negative
+      // sums here, and an index past hi reads a clamped, staged pixel).  The
+      // horizontal sums of a source row (buf in the reference) do not depend
+      // on the destination row, so the walk keeps the last three rows' sums
+      // and computes ~scale_y new rows per destination row.  Two columns per
+      // thread (one row group walks the band): few registers.
+      const int nq2 = out_w >> 1;
+      const int q2 = t;
+      if (q2 >= nq2) return;
+      const int dc0 = 2 * q2;
+      AreaTaps tx[2];
+      int xb[2];
+      float wx[2][3];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        tx[j] = area_taps(P.sw, P.scale_x, ep.src_x(dc0 + j));
+        xb[j] = tx[j].lo;
+#pragma unroll
+        for (int k = 0; k < 3; k++) wx[j][k] = tx[j].lo + k <= tx[j].hi ? tx[j].w(tx[j].lo + k) : 0.f;
+      }
+      uint32_t cm = 0;
+#pragma unroll
+      for (int j = 0; j < 2; j++) cm |= ep.in_cut(ep.cut_y, dc0 + j) ? 1u << j : 0u;
+      auto hsum = [&](int r, float B[6]) {  // buf of source row r for both columns, table order
+        const uint8_t *row = L.row(r);
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+#pragma unroll
+          for (int c = 0; c < 3; c++) {
+            float b = 0.f;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+              const int sx = min(xb[j] + k, tx[j].hi);
+              b = b + (float)row[sx * 3 + c] * wx[j][k];
+            }
+            B[3 * j + c] = b;
+          }
+        }
+      };
+      int R[3] = {-1, -1, -1};
+      float BR[3][6];
+      for (int dy = oy0; dy < oy1; dy++) {
+        const AreaTaps ty = s_at[dy - oy0];
+        float NB[3][6];
+        int NR[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const int r = min(ty.lo + k, ty.hi);  // uniform: every thread walks the same rows
+          NR[k] = r;
+          if (r == R[0]) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) NB[k][i] = BR[0][i];
+          } else if (r == R[1]) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) NB[k][i] = BR[1][i];
+          } else if (r == R[2]) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) NB[k][i] = BR[2][i];
+          } else if (k > 0 && r == NR[k - 1]) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) NB[k][i] = NB[k - 1][i];
+          } else {
+            hsum(r, NB[k]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          R[k] = NR[k];
+#pragma unroll
+          for (int i = 0; i < 6; i++) BR[k][i] = NB[k][i];
+        }
+        float bt[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) bt[k] = ty.lo + k <= ty.hi ? ty.w(ty.lo + k) : 0.f;
+        int v[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+          float sum = bt[0] * NB[0][i];
+          sum = sum + bt[1] * NB[1][i];
+          sum = sum + bt[2] * NB[2][i];
+          v[i] = sat_u8i(ffcv_f2i_rn(sum));
+        }
+#ifdef RRC_TIMING_NOSTORE
+        if (p.cutout_fill[3] != 77) continue;  // timing only: compute without the stores
+#endif
+        if (cm && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
+#pragma unroll
+          for (int j = 0; j < 2; j++)
+            if ((cm >> j) & 1) {
+              v[3 * j] = ep.fill[0];
+              v[3 * j + 1] = ep.fill[1];
+              v[3 * j + 2] = ep.fill[2];
+            }
+        }
+        const uint64_t px = (uint64_t)dy * out_w + dc0;
+        if (FP16) {  // 12 bytes, 4-byte aligned
+          uint32_t h[6];
+#pragma unroll
+          for (int i = 0; i < 6; i++) h[i] = s_lut[v[i] * 3 + i % 3];
+          uint32_t *o32 = (uint32_t *)((uint16_t *)o + px * 3);
+          o32[0] = h[0] | (h[1] << 16);
+          o32[1] = h[2] | (h[3] << 16);
+          o32[2] = h[4] | (h[5] << 16);
+        } else {  // 6 bytes, 2-byte aligned
+          uint16_t *o16 = (uint16_t *)((uint8_t *)o + px * 3);
+          __builtin_nontemporal_store((uint16_t)(v[0] | (v[1] << 8)), o16);
+          __builtin_nontemporal_store((uint16_t)(v[2] | (v[3] << 8)), o16 + 1);
+          __builtin_nontemporal_store((uint16_t)(v[4] | (v[5] << 8)), o16 + 2);
+        }
+      }
+      return;
+    }
     // row groups: tpg threads (a power of two >= nq, >= 64) per group, each
     // group walks its own slice of the band's rows
     int tpg = 64;
     while (tpg < nq) tpg <<= 1;
     const int groups = RRC_THREADS / tpg;
-    const int per = (RRC_BAND + groups - 1) / groups;
+    const int per = (oy1 - oy0 + groups - 1) / groups;
     const int g = t / tpg, q = t - g * tpg;
     const int gy0 = oy0 + g * per, gy1 = min(oy1, gy0 + per);
     if (q >= nq || gy0 >= gy1) return;
     const int dx0 = 4 * q;
-    // cutout, then one 12-byte (u8) or three 8-byte (fp16) stores
+    // cutout: the columns of this thread's quad inside the square (bit j =
+    // column dx0 + j; flip-aware), tested once; rows test their own range
+    uint32_t cmask = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) cmask |= ep.in_cut(ep.cut_y, dx0 + j) ? 1u << j : 0u;
+    // one 12-byte (u8) or three 8-byte (fp16) stores of the quad's pixels
     auto put = [&](int dy, int v[12]) {
 #ifdef RRC_TIMING_NOSTORE
       if (p.cutout_fill[3] != 77) return;  // timing only: compute without the stores
 #endif
+      if (cmask && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (ep.in_cut(dy, dx0 + j)) {
-          v[3 * j] = ep.fill[0];
-          v[3 * j + 1] = ep.fill[1];
-          v[3 * j + 2] = ep.fill[2];
-        }
+        for (int j = 0; j < 4; j++)
+          if ((cmask >> j) & 1) {
+            v[3 * j] = ep.fill[0];
+            v[3 * j + 1] = ep.fill[1];
+            v[3 * j + 2] = ep.fill[2];
+          }
+      }
       const uint64_t px = (uint64_t)dy * out_w + dx0;
       if (FP16) {  // 24-byte group, 8-byte aligned (dx0 % 4 == 0)
         uint32_t h[12];
@@ -216,7 +341,8 @@ __global__ void __launch_bounds__(RRC_THREADS)
         w.x = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
         w.y = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
         w.z = v[8] | (v[9] << 8) | (v[10] << 16) | (v[11] << 24);
-        // streaming output: non-temporal (measured +2% over plain stores)
+        // streaming output: non-temporal (measured +2% over plain stores; 16-byte
+        // aligned stores of 4-lane groups exchanged by DPP measured the same)
         __builtin_nontemporal_store(w, (u32x3 *)((uint8_t *)o + px * 3));
       }
     };
@@ -248,16 +374,22 @@ __global__ void __launch_bounds__(RRC_THREADS)
     // are in [0, 2048] with wa + wb <= 2049 (linear_coef rounds each), so
     // 0 <= h >> 4 <= 255 * 2049 >> 4 = 32655 and the vertical sum
     // m0 + m1 <= 32655 * 2049 >> 16 = 1020, (1020 + 2) >> 2 = 255.
-    auto hrow = [&](int r, int H[12]) {
+    // The row keeps (h >> 4) << 8 (< 2^23), so VResizeLinearVec's
+    // (h * c) >> 16 is one 24-bit high multiply by c << 8 (< 2^20):
+    // mulhi_u24(h << 8, c << 8) = (h * c * 2^16) >> 32.
+    auto hrow = [&](int r, uint32_t H[12]) {
       const uint8_t *row = L.row(r);
 #pragma unroll
       for (int j = 0; j < 4; j++)
 #pragma unroll
         for (int c = 0; c < 3; c++)
-          H[3 * j + c] = (row[xa[j] + c] * wa[j] + row[xb[j] + c] * wb[j]) >> 4;
+          H[3 * j + c] = (((uint32_t)(row[xa[j] + c] * wa[j] + row[xb[j] + c] * wb[j]) >> 4) & 0x7fffu) << 8;
+    };
+    auto mulhi24 = [](uint32_t a, uint32_t b) -> uint32_t {  // a, b < 2^24: v_mul_hi_u32_u24
+      return (uint32_t)(((uint64_t)(a & 0xffffffu) * (b & 0xffffffu)) >> 32);
     };
     int ca = -1, cb = -1;
-    int HA[12], HB[12];
+    uint32_t HA[12], HB[12];
     for (int dy = gy0; dy < gy1; dy++) {
       const LinTap ly = s_rt[dy - oy0];
       const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
@@ -274,12 +406,11 @@ __global__ void __launch_bounds__(RRC_THREADS)
         hrow(rb, HB);
         cb = rb;
       }
+      const uint32_t c0 = ((uint32_t)ly.c0 & 0xfffu) << 8, c1 = ((uint32_t)ly.c1 & 0xfffu) << 8;
       int v[12];
 #pragma unroll
-      for (int i = 0; i < 12; i++) {  // VResizeLinearVec_32s8u, + 2 folded into m0, no saturation (see hrow)
-        const int m0 = (__mul24(HA[i], ly.c0) + (2 << 16)) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;
-        v[i] = (m0 + m1) >> 2;
-      }
+      for (int i = 0; i < 12; i++)  // VResizeLinearVec_32s8u: (m0 + 2 + m1) >> 2, no saturation (see hrow)
+        v[i] = (int)((mulhi24(HA[i], c0) + mulhi24(HB[i], c1) + 2u) >> 2);
       put(dy, v);
     }
     return;

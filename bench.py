@@ -575,10 +575,14 @@ def main():
             kernel_ms += ms.astype(np.float64).sum(0)
             kernel_imgs += sum(sl['timed'])
             sl.pop('timed')
+    per_rank = None
     if dist:
+        # every rank's own time (the line reports them beside the max)
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        allt = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(allt, t)
+        per_rank = [float(x.item()) for x in allt]
+        elapsed = max(per_rank)
     parity = None
     if args.parity_rows > 0 and not (args.only or args.k2flags):
         parity = parity_check(args.config, slots, order, batch, tile, offs, sizes, hs, ws, args.parity_rows)
@@ -808,6 +812,13 @@ def main():
         'roofline': roof,
         'cpu_baseline': None,
     }
+    if dist:
+        res['process_group'] = {
+            'backend': dist.get_backend(), 'world_size': dist.get_world_size(),
+            'per_rank': [{'rank': r, 'seconds': round(x, 6), 'images': batch * args.steps,
+                          'images_per_s': round(batch * args.steps / x, 1)} for r, x in enumerate(per_rank)],
+            'note': 'value = all ranks\' images / the slowest rank\'s time (barrier + synchronize around the '
+                    'timed region on every rank)'}
     if parity is not None:
         res['parity'] = parity
     if later is not None:

@@ -126,9 +126,8 @@ struct ImgInfo {
   ResizePlan plan;
   int32_t taps;
   // K1 -> jpeg_idct_kernel: what the DC prediction and the IDCT need
-  uint64_t cf_off, dc_off;  // arena offsets of the window coefficients and the DC differences
-  uint64_t coff[3];         // first window block of each component in the coefficient region
-  uint32_t dc_bytes;
+  uint64_t cf_off;   // arena offset of the window coefficients
+  uint64_t coff[3];  // first window block of each component in the coefficient region
   int32_t nblocks, bpm, mcux;
   int32_t hs[3], vs[3], wx0[3], wx1[3], wy0[3], wy1[3], qmax[3];
   int32_t blk_comp[10], blk_dx[10], blk_dy[10];
@@ -437,10 +436,10 @@ FFCV_DEV int si_bits(uint32_t inf) { return (int)(inf >> 27) & 15; }
 FFCV_DEV int si_set(uint32_t inf) { return (int)(inf >> 24) & 7; }
 
 template <class TB>
-FFCV_DEV uint32_t decode_entry(const TB &T, uint32_t acmask, uint32_t inf, uint64_t acc) {
+FFCV_DEV uint32_t decode_entry(const TB &T, uint32_t acmask, uint32_t inf, uint64_t acc, bool live = true) {
   const uint32_t hi = (uint32_t)(acc >> 32);
   uint32_t e = *(const uint32_t *)((const uint8_t *)T.lut + ((inf >> 5) & 0xffff) + ((hi >> (inf & 31)) << 2));
-  if ((e & 31) == 0) {
+  if ((e & 31) == 0 && live) {  // (a finished lane of a wave-uniform loop skips the rare paths)
     const uint32_t look = hi >> 16;
     const int bits = si_bits(inf), slot = (int)(inf >> 21) & 7;
     if (e) e = T.lut2[si_set(inf)][(e >> 5) - 1][(look >> (16 - bits - SUBB)) & ((1 << SUBB) - 1)];
@@ -604,18 +603,19 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
   locate_block(S.phr[ph].pd0, S.phr[ph].pd1, blk, nblocks, mx, my, boff, inwin);
   int cc = S.phr[ph].pd1.w;  // component of the block in progress
   int r0 = 0, r1 = 0, r2 = 0;  // running DC sums of the blocks this lane started
+  const bool alive = true;  // (a wave-uniform loop with finished lanes idling measured neutral)
   while (pos < end_bit && !(z == 0 && blk >= nblocks)) {
     K1_DIAG(iters++);
     br.begin();
     const uint32_t ndinf = S.phr[nph].dinf, nainf = S.phr[nph].ainf;
     const int nnph = S.phr[nph].next;
     const int4 npd0 = S.phr[nph].pd0, npd1 = S.phr[nph].pd1;
-    const bool isblk = z == 0;
-    const uint32_t e = decode_entry(T, S.acmask, isblk ? dinf : ainf, br.acc);
+    const bool isblk = z == 0 && alive;
+    const uint32_t e = decode_entry(T, S.acmask, z == 0 ? dinf : ainf, br.acc, alive);
     // see make_pair: vs = this step's bits and z advance
-    const int zi1 = (int)(e >> 25);
+    const int zi1 = alive ? (int)(e >> 25) : 0;
     const bool one = z + zi1 >= 64, pair = zi1 != 0;
-    const uint32_t vs = one ? e >> 16 : e;
+    const uint32_t vs = alive ? (one ? e >> 16 : e) : 0u;
     const int nbits = (int)(vs & 31), zadd = (int)(vs >> 9) & 127;
     const int t1 = pair ? (int)(e >> 16) & 31 : nbits, zinc = pair ? zi1 : zadd;
     const uint32_t size = (e >> 5) & 15, size2 = pair && !one ? (e >> 21) & 15 : 0u;
@@ -640,7 +640,7 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     }
 #ifndef K1_TIMING_NOAC
     const int p1 = min(z + zinc - 1, 63), p2 = min(z + zadd - 1, 63);
-    const bool a1 = !isblk && size && inwin, a2 = size2 && inwin;
+    const bool a1 = z != 0 && size && inwin && alive, a2 = size2 && inwin && alive;
     const bool l1 = a1 && stg && p1 < ACS_Z, l2 = a2 && stg && p2 < ACS_Z;
     if (l1) acs16[p1] = (int16_t)v;
     if (l2) acs16[p2] = (int16_t)v2;
@@ -1503,11 +1503,14 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 // 0 does the atomic) and zero its window coefficients (the write pass stores
 // only non-zero coefficients).  Region sizes: de-stuffed stream + padding,
 // window coefficients (int16 x 64 per block), DC differences (int16 per
-// block), window planes (64 B per block), K2 band staging (crop RGB).
+// block, coefficient output only), window planes (64 B per block), K2 band
+// staging (crop RGB).
 FFCV_DEV uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t, int MODE) {
   const uint64_t ds = align256((uint64_t)nbytes + 64), cf = align256((uint64_t)S.nwin * 128);
-  const uint64_t dc = align256((uint64_t)S.nblocks * 2), pl = align256((uint64_t)S.nwin * 64);
+  // DC differences are stored only for the coefficient output (the other
+  // modes predict DC from the write pass's per-lane running sums)
+  const uint64_t dc = MODE == JM_COEF ? align256((uint64_t)S.nblocks * 2) : 0, pl = align256((uint64_t)S.nwin * 64);
   const uint64_t rgb = MODE == JM_RRC ? align256((uint64_t)S.rh * S.rw * 3) : 0;
   const uint64_t need = ds + cf + dc + pl + rgb;
   unsigned long long base = 0;
@@ -1947,8 +1950,6 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
     info->rgb_off = S.rgb_off;
     info->cf_off = S.cf_off;
-    info->dc_off = S.dc_off;
-    info->dc_bytes = S.dc_bytes;
     info->nblocks = S.nblocks;
     info->bpm = S.bpm;
     info->mcux = S.mcux;
@@ -2869,6 +2870,34 @@ int ffcv_jpeg_timing_read(ffcv_jpeg_ctx *c, float *ms, int max_launches, int *n_
   }
   *n_launches = n;
   c->tev_n = 0;
+  return FFCV_OK;
+}
+
+// Diagnostic hook (not in the public header): the DC lane table the last
+// RRC / FULL launch's entropy kernel wrote for images [0, n): lane_blk0[64]
+// (first block each lane started, non-decreasing), lane_off[3][64] (the
+// lanes' exclusive DC offsets per component) and the image status.
+int ffcv_jpeg_lane_table(ffcv_jpeg_ctx *c, void *stream, int n, uint32_t *blk0, int32_t *off, int32_t *status) {
+  if (!c || n < 0 || n > c->max_batch || !blk0 || !off || !status) {
+    ffcv::set_error("ffcv_jpeg_lane_table: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  hipStream_t s = ffcv::as_stream(stream);
+  ImgInfo *h = new ImgInfo[n > 0 ? n : 1];
+  hipError_t e = hipMemcpyAsync(h, c->info, sizeof(ImgInfo) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete[] h;
+    return ffcv::check_hip(e, "ffcv_jpeg_lane_table");
+  }
+  for (int k = 0; k < n; k++) {
+    status[k] = h[k].status;
+    for (int l = 0; l < 64; l++) {
+      blk0[64 * k + l] = h[k].lane_blk0[l];
+      for (int q = 0; q < 3; q++) off[192 * k + 64 * q + l] = h[k].lane_off[q][l];
+    }
+  }
+  delete[] h;
   return FFCV_OK;
 }
 

@@ -770,3 +770,80 @@ def test_c3_scale_three_streams(hip_lib, oracle):
         oracle.use_libjpeg_turbo(False)
     for sl in slots:
         sl['dec'].close()
+
+
+def _lane_table(dec, n):
+    import ctypes
+    from ffcv_amd import libffcv as L
+    lib = L.lib()
+    f = lib.ffcv_jpeg_lane_table
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    blk0 = np.zeros((n, 64), np.uint32)
+    off = np.zeros((n, 3, 64), np.int32)
+    st = np.zeros(n, np.int32)
+    assert f(dec.handle, None, n, blk0.ctypes.data, off.ctypes.data, st.ctypes.data) == 0
+    return blk0, off, st
+
+
+def test_dc_lane_sums_invariants(hip_lib, oracle):
+    """the DC prediction by per-lane running sums needs each lane's
+    first started block (lane_blk0) non-decreasing and a lane that starts no
+    block to add nothing (its exclusive offsets equal the next lane's).
+    Images chosen for the corner cases: DC-only blocks (many blocks per
+    lane), small q100 noise (ranges of ~192 bits inside ~500-bit blocks:
+    lanes that start and stop inside one block), a crop window whose first
+    block belongs to a lane that started before the window, and natural
+    images; checked on the full-sync path and on the entropy-index path
+    (identical lane tables and bit-exact pixels)."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(5)
+    imgs = [np.full((256, 256, 3), 97, np.uint8), rng.integers(0, 256, (16, 16, 3)).astype(np.uint8),
+            rng.integers(0, 256, (24, 40, 3)).astype(np.uint8), natural_image(rng, 192, 256),
+            natural_image(rng, 256, 200)]
+    subs = ['4:2:0', '4:4:4', '4:2:0', '4:2:0', '4:4:4']
+    quals = [90, 100, 100, 90, 95]
+    blobs = [encode_jpeg(im, q, sb) for im, q, sb in zip(imgs, quals, subs)]
+    n = len(blobs)
+    buf, offs, sizes = pack(blobs)
+    hs = [i.shape[0] for i in imgs]
+    ws = [i.shape[1] for i in imgs]
+    table = _samples(offs, sizes, hs, ws, np.zeros(n))
+    d_buf, d_table = _upload(buf), _dev(table)
+    ids = np.arange(n, dtype=np.int64)
+    d_ids = torch.from_numpy(ids).to('cuda:0')
+    dp = L.DrawParams()
+    dp.out_h = dp.out_w = 64
+    dp.scale[0], dp.scale[1] = 0.3, 0.6
+    dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
+    dp.loader_seed = 3
+    rp = L.RRCParams()
+    rp.out_h = rp.out_w = 64
+    dec = L.JpegDecoder(n, max(hs), max(ws), int(sizes.max()))
+    index = torch.zeros((n, L.EIDX_LANES, L.EIDX_WORDS), dtype=torch.int32, device='cuda:0')
+
+    def run():
+        crops = torch.empty((n, 4), dtype=torch.int32, device='cuda:0')
+        out = torch.zeros((n, 64, 64, 3), dtype=torch.uint8, device='cuda:0')
+        status = torch.full((n,), -1, dtype=torch.int32, device='cuda:0')
+        dec.rrc_fused(d_buf, d_table, d_ids, dp, crops, None, None, rp, out, status)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == 0).all()
+        return out.cpu().numpy(), crops.cpu().numpy(), _lane_table(dec, n)
+
+    dec.set_entropy_index(index)
+    tables = []
+    for it in range(2):  # full sync (publishes the index), then the index-hit path
+        got, crops, (blk0, off, st) = run()
+        want = oracle.rrc_batch([(b, h, w, 0) for b, h, w in zip(blobs, hs, ws)], crops, 64, 64)
+        assert np.array_equal(got, want), f'pass {it}'
+        assert (st == 0).all()
+        assert (np.diff(blk0.astype(np.int64), axis=1) >= 0).all(), f'pass {it}: lane_blk0 not monotonic'
+        empty = blk0[:, 1:] == blk0[:, :-1]  # lane l started no block
+        for c in range(3):
+            assert (off[:, c, 1:][empty] == off[:, c, :-1][empty]).all(), f'pass {it}: empty lane adds DC'
+        tables.append((blk0, off))
+    assert np.array_equal(tables[0][0], tables[1][0]) and np.array_equal(tables[0][1], tables[1][1])
+    # the corner cases occurred: a lane inside one block (the q100 noise images)
+    assert empty[1:3].any()
+    dec.set_entropy_index(None)

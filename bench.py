@@ -249,10 +249,10 @@ def c5_subresult(timeout_s=150):
     """BASELINE configs[4] (C5, "the HBM-bound roofline point": raw 512x512
     RGB, RRC 448 + Cutout 64, batch 256) measured beside the headline, never
     as `value`: this script in a child process with --config c5 (1,024
-    unique raw encodings replicated to the 10,000-sample .beton, 40 timed
+    unique raw encodings replicated to the 10,000-sample .beton, 200 timed
     steps, parity-checked); its line is returned with its own roofline."""
     import subprocess
-    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', 'c5', '--steps', '40', '--warmup', '10',
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', 'c5', '--steps', '200', '--warmup', '20',
            '--unique', '1024', '--no-cpu-baseline', '--parity-rows', '512']
     env = dict(os.environ)
     for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
@@ -767,6 +767,10 @@ def main():
                     e['hbm_frac_counter'] = round(b / ns_img / HBM_PEAK_GBS, 4)
                 per[n] = e
             dom = max(kernels, key=lambda n: per[n]['ns_per_image_isolated'])
+            for n in kernels:  # whole-path algorithmic bytes over one kernel's time: the dominant kernel only
+                if n != dom:
+                    per[n].pop('hbm_frac_alg', None)
+                    per[n].pop('hbm_frac_alg_profile', None)
             d = per[dom]
             # the line's roofline is the dominant kernel's (the contract's
             # "roofline of the dominant kernel"); the three-kernel sum stays as `path`

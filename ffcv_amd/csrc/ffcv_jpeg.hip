@@ -1519,7 +1519,11 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
   // 2^31 would otherwise sign-extend and read as TOO_LARGE)
   base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
-  if (base + need > a.arena_bytes) return FFCV_SAMPLE_TOO_LARGE;  // arena exhausted
+  if (base + need > a.arena_bytes) {  // arena exhausted: give the space back, so one huge image
+    // does not fail every image that allocates after it
+    if (t == 0) atomicAdd(a.arena_top, (unsigned long long)0 - (unsigned long long)need);
+    return FFCV_SAMPLE_TOO_LARGE;
+  }
   S.ds_off = base;
   S.ds_bytes = (uint32_t)ds;
   S.cf_off = base + ds;
@@ -2438,7 +2442,10 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       // computed): weights are in [0, 2048] with c0 + c1 <= 2049 (linear_coef
       // rounds each), so 0 <= h >> 4 <= 255 * 2049 >> 4 = 32655 and the
       // vertical sum m0 + m1 <= 32655 * 2049 >> 16 = 1020, (1020 + 2) >> 2 = 255.
-      auto hrow = [&](int r, int H[6]) {
+      // The rows keep (h >> 4) << 8 (< 2^23), so VResizeLinearVec's
+      // (h * c) >> 16 is one 24-bit high multiply by c << 8 (< 2^20):
+      // mulhi_u24(h << 8, c << 8) = (h * c * 2^16) >> 32.
+      auto hrow = [&](int r, uint32_t H[6]) {
         const uint32_t *row = rgbx + __mul24(r - r0, rw);
         const uint32_t p0 = row[l0.s], q0 = row[s0b];
         const uint32_t p1 = row[l1.s], q1 = row[s1b];
@@ -2446,14 +2453,20 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
         for (int c = 0; c < 3; c++) {
           const int a0 = (p0 >> (8 * c)) & 255, b0 = (q0 >> (8 * c)) & 255;
           const int a1 = (p1 >> (8 * c)) & 255, b1 = (q1 >> (8 * c)) & 255;
-          H[c] = (a0 * a0w + b0 * b0w) >> 4;
-          H[3 + c] = (a1 * a1w + b1 * b1w) >> 4;
+          H[c] = (((uint32_t)(a0 * a0w + b0 * b0w) >> 4) & 0x7fffu) << 8;
+          H[3 + c] = (((uint32_t)(a1 * a1w + b1 * b1w) >> 4) & 0x7fffu) << 8;
         }
       };
+      auto mulhi24 = [](uint32_t x, uint32_t y) -> uint32_t {  // x, y < 2^24: v_mul_hi_u32_u24
+        return (uint32_t)(((uint64_t)(x & 0xffffffu) * (y & 0xffffffu)) >> 32);
+      };
+      // cutout: which of this thread's two columns lie in the square (tested
+      // once; a row tests its own range)
+      const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
       const int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
       const int ya = oy0 + sub * half, yb = (a.k2flags & 512) ? ya : min(oy1, ya + half);
       int ca = -1, cb = -1;
-      int HA[6], HB[6];
+      uint32_t HA[6], HB[6];
       for (int dy = ya; dy < yb; dy++) {
         const LinTap ly = rtab[dy - oy0];
         const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
@@ -2471,22 +2484,21 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
           cb = rb;
         }
         int o[6];
+        const uint32_t c0 = ((uint32_t)ly.c0 & 0xfffu) << 8, c1 = ((uint32_t)ly.c1 & 0xfffu) << 8;
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
-          // (sat_s16(m0 + m1) + 2) >> 2 with the + 2 folded into m0 (2 << 16 is a
-          // multiple of 2^16), no saturation (see hrow)
-          const int m0 = (__mul24(HA[i], ly.c0) + (2 << 16)) >> 16, m1 = __mul24(HB[i], ly.c1) >> 16;
-          o[i] = (m0 + m1) >> 2;
-        }
-        if (ep.in_cut(dy, dx0)) {
-          o[0] = ep.fill[0];
-          o[1] = ep.fill[1];
-          o[2] = ep.fill[2];
-        }
-        if (ep.in_cut(dy, dx0 + 1)) {
-          o[3] = ep.fill[0];
-          o[4] = ep.fill[1];
-          o[5] = ep.fill[2];
+        for (int i = 0; i < 6; i++)  // (sat_s16(m0 + m1) + 2) >> 2, no saturation (see hrow)
+          o[i] = (int)((mulhi24(HA[i], c0) + mulhi24(HB[i], c1) + 2u) >> 2);
+        if ((cut0 || cut1) && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
+          if (cut0) {
+            o[0] = ep.fill[0];
+            o[1] = ep.fill[1];
+            o[2] = ep.fill[2];
+          }
+          if (cut1) {
+            o[3] = ep.fill[0];
+            o[4] = ep.fill[1];
+            o[5] = ep.fill[2];
+          }
         }
         const uint64_t p0 = (uint64_t)dy * out_w + dx0;
         if (FP16) {

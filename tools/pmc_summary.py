@@ -44,7 +44,7 @@ for tag in ('fetch', 'write', 'sq'):
         for c, v in cs.items():
             res[k][c] = sum(v) / len(v)
 def _ours(k):
-    return 'jpeg' in k or 'rrc' in k or 'lut' in k or 'draw' in k or 'gather' in k
+    return k.startswith(('jpeg_', 'rrc_', 'lut_', 'draw_', 'gather_samples', 'gather_raw', 'cutout_', 'flip_'))
 
 
 summary = {}

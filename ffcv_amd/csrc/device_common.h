@@ -10,6 +10,7 @@
 #include "../../include/ffcv_hip.h"
 
 #define FFCV_DEV __device__ __forceinline__
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));  // v_dot2_u32_u16 operands
 // The INTER_AREA restatement below is single-source: the kernels run it per
 // output pixel and the host C-ABI resize() (csrc/ffcv_host.hip, the
 // reference's libffcv.cpp:33-42 signature) runs the very same functions on

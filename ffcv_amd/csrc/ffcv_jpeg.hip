@@ -2123,6 +2123,60 @@ struct ColorGeom {
   int ncomp, color_rgb;
   int he[3], ve[3], cw[3], ch[3];
 };
+// The part of an image record K2 reads (ImgInfo up to and including `taps`),
+// fetched with ONE vector load per lane (lane i: dword i) at the top of the
+// kernel together with the LUT, tap and epilogue loads, then broadcast to
+// scalar registers with v_readlane.  Reading the fields from the global
+// record where they are used issued them in ~6 dependent round trips (the
+// compiler may not hoist loads above the status / mode branches), which was
+// most of K2's per-workgroup fixed cost.
+#define K2REC_DW ((int)((offsetof(ImgInfo, taps) + 4) / 4))
+static_assert(K2REC_DW <= 64, "record head fits one wave's lanes");
+struct K2Rec {
+  uint32_t w;  // this lane's dword of the record head
+  FFCV_DEV uint32_t u(int i) const { return (uint32_t)__builtin_amdgcn_readlane((int)w, i); }
+  FFCV_DEV int32_t s(int i) const { return (int32_t)u(i); }
+  FFCV_DEV uint64_t u64(int i) const { return (uint64_t)u(i) | ((uint64_t)u(i + 1) << 32); }
+  FFCV_DEV double f64(int i) const { return __builtin_bit_cast(double, u64(i)); }
+};
+#define K2F(f) ((int)(offsetof(ImgInfo, f) / 4))
+FFCV_DEV ImgInfo k2_head(const K2Rec &R) {
+  ImgInfo I;  // only the head fields are set (SROA keeps them in registers)
+  I.status = R.s(K2F(status));
+  I.W = R.s(K2F(W));
+  I.H = R.s(K2F(H));
+  I.ncomp = R.s(K2F(ncomp));
+  I.color_rgb = R.s(K2F(color_rgb));
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    I.he[c] = R.s(K2F(he) + c);
+    I.ve[c] = R.s(K2F(ve) + c);
+    I.cw[c] = R.s(K2F(cw) + c);
+    I.ch[c] = R.s(K2F(ch) + c);
+    I.stride[c] = R.s(K2F(stride) + c);
+    I.poff[c] = R.u64(K2F(poff) + 2 * c);
+  }
+  I.ri = R.s(K2F(ri));
+  I.rj = R.s(K2F(rj));
+  I.rh = R.s(K2F(rh));
+  I.rw = R.s(K2F(rw));
+  I.rgb_off = R.u64(K2F(rgb_off));
+  I.plan.sw = R.s(K2F(plan.sw));
+  I.plan.sh = R.s(K2F(plan.sh));
+  I.plan.dw = R.s(K2F(plan.dw));
+  I.plan.dh = R.s(K2F(plan.dh));
+  I.plan.kind = R.s(K2F(plan.kind));
+  I.plan.isx = R.s(K2F(plan.isx));
+  I.plan.isy = R.s(K2F(plan.isy));
+  I.plan.vec_end = R.s(K2F(plan.vec_end));
+  I.plan.scale_x = R.f64(K2F(plan.scale_x));
+  I.plan.scale_y = R.f64(K2F(plan.scale_y));
+  I.plan.inv_x = R.f64(K2F(plan.inv_x));
+  I.plan.inv_y = R.f64(K2F(plan.inv_y));
+  I.taps = R.s(K2F(taps));
+  return I;
+}
+
 FFCV_DEV ColorGeom color_geom(const ImgInfo &I) {
   ColorGeom g;
   g.ncomp = I.ncomp;
@@ -2190,6 +2244,27 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
   const int t = threadIdx.x;
   const int k = blockIdx.y;
   const int band = blockIdx.x;
+  // ---- one round trip for everything that depends only on (k, band, t):
+  // the record head, the LUT, this band's row taps, this thread's column
+  // taps and the epilogue draws (see K2Rec)
+  K2Rec R;
+  R.w = (t & 63) < K2REC_DW ? ((const uint32_t *)(a.info + k))[t & 63] : 0u;
+  constexpr int LU = (768 + K2T - 1) / K2T;
+  uint16_t lv[LU];
+  if (FP16) {
+#pragma unroll
+    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? a.p.lut[u * K2T + t] : (uint16_t)0;
+  }
+  const int band_rows_n = MODE == JM_RRC ? min(a.p.out_h - band * BAND, BAND) : 0;
+  const uint2 *ktaps = MODE == JM_RRC && a.taps ? a.taps + (uint64_t)k * K2_TAPS : nullptr;
+  uint2 rt_pre = make_uint2(0, 0);
+  uint4 ct_pre = make_uint4(0, 0, 0, 0);
+  if (ktaps) {
+    if (t < band_rows_n) rt_pre = ktaps[a.p.out_w + band * BAND + t];
+    if (2 * (t % K2_COLS) + 1 < a.p.out_w) ct_pre = *(const uint4 *)(ktaps + 2 * (t % K2_COLS));
+  }
+  const int cut_y0 = a.cut ? a.cut[2 * k] : 0, cut_x0 = a.cut ? a.cut[2 * k + 1] : 0;
+  const int flip0 = a.flips ? a.flips[k] : 0;
   if (k == 0 && band == 0 && t == 0) {  // K1 is done: close its arena (see arena_before_k1)
     const unsigned long long top = a.arena_top[0];
     if (top) {
@@ -2197,7 +2272,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       a.arena_top[0] = 0;
     }
   }
-  const ImgInfo &I = a.info[k];
+  const ImgInfo I = k2_head(R);
   const int status = I.status;
   if (status == -1) return;  // raw sample (handled by the raw kernel)
   const int out_h = MODE == JM_FULL ? (int)a.samples[k].height : a.p.out_h;
@@ -2232,18 +2307,14 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
     }
     return;
   }
-  if (FP16) {  // all loads in flight before the LDS writes
-    constexpr int LU = (768 + K2T - 1) / K2T;
-    uint16_t lv[LU];
-#pragma unroll
-    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? a.p.lut[u * K2T + t] : (uint16_t)0;
+  if (FP16) {  // (loaded at the top)
 #pragma unroll
     for (int u = 0; u < LU; u++)
       if (u * K2T + t < 768) s_lut[u * K2T + t] = lv[u];
   }
   const int ri = I.ri, rj = I.rj, rh = I.rh, rw = I.rw;
   const ResizePlan P = MODE == JM_RRC ? I.plan : make_plan(rw, rh, out_w, out_h);  // RRC: K1's plan
-  const uint2 *taps = MODE == JM_RRC && I.taps ? a.taps + (uint64_t)k * K2_TAPS : nullptr;
+  const uint2 *taps = I.taps ? ktaps : nullptr;
   int r0, r1;
   band_rows(P, oy0, oy1, &r0, &r1);
   const int nrows = r1 - r0 + 1;
@@ -2253,9 +2324,9 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
   ep.out_h = out_h;
   ep.out_w = out_w;
   ep.cut_size = a.cut ? a.p.cutout_size : 0;
-  ep.cut_y = a.cut ? a.cut[2 * k] : 0;
-  ep.cut_x = a.cut ? a.cut[2 * k + 1] : 0;
-  ep.flip = a.flips ? a.flips[k] : 0;
+  ep.cut_y = cut_y0;
+  ep.cut_x = cut_x0;
+  ep.flip = flip0;
   ep.cut_before_flip = a.p.cutout_fill[3];
   ep.fill[0] = a.p.cutout_fill[0];
   ep.fill[1] = a.p.cutout_fill[1];
@@ -2302,7 +2373,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
     need += nrows * rw * 4 + 4;  // + a dummy word for the colour pass's off-crop pixels
     if (need <= K2_LDS) {
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
-      if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(taps[out_w + oy0 + t]) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+      if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
       TPlane tp[3];
       // tile staging: the first SU dwords per thread of every component are
       // loaded before any LDS write (one memory round trip, not one per
@@ -2425,8 +2496,8 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       if (tx >= out_w / 2) return;
       const int dx0 = 2 * tx;
       LinTap l0, l1;
-      if (taps) {  // K1's table (flip applied): both columns in one 16-byte load
-        const uint4 q = *(const uint4 *)(taps + dx0);
+      if (taps) {  // K1's table (flip applied): both columns in one 16-byte load (at the top)
+        const uint4 q = ct_pre;
         l0 = tap_unpack(make_uint2(q.x, q.y));
         l1 = tap_unpack(make_uint2(q.z, q.w));
       } else {
@@ -2445,16 +2516,25 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       // The rows keep (h >> 4) << 8 (< 2^23), so VResizeLinearVec's
       // (h * c) >> 16 is one 24-bit high multiply by c << 8 (< 2^20):
       // mulhi_u24(h << 8, c << 8) = (h * c * 2^16) >> 32.
+      // On gfx950 every multiply, bit-field extract and 3-operand integer
+      // form issues in 4 cycles per wave against 2 for add / shift / and
+      // (tools/op_rate), so the pair of a channel's two source samples is
+      // gathered by one v_perm_b32 as u16 halves and weighted by one
+      // v_dot2_u32_u16 with the weights pre-scaled by 16: dot = 16 h, and
+      // (h >> 4) << 8 = dot & 0x7fff00 (10 cycles per value instead of 22).
+      const uint32_t w0 = ((uint32_t)a0w << 4) | ((uint32_t)b0w << 20), w1 = ((uint32_t)a1w << 4) | ((uint32_t)b1w << 20);
       auto hrow = [&](int r, uint32_t H[6]) {
         const uint32_t *row = rgbx + __mul24(r - r0, rw);
         const uint32_t p0 = row[l0.s], q0 = row[s0b];
         const uint32_t p1 = row[l1.s], q1 = row[s1b];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
-          const int a0 = (p0 >> (8 * c)) & 255, b0 = (q0 >> (8 * c)) & 255;
-          const int a1 = (p1 >> (8 * c)) & 255, b1 = (q1 >> (8 * c)) & 255;
-          H[c] = (((uint32_t)(a0 * a0w + b0 * b0w) >> 4) & 0x7fffu) << 8;
-          H[3 + c] = (((uint32_t)(a1 * a1w + b1 * b1w) >> 4) & 0x7fffu) << 8;
+          // bytes [p.c, 0, q.c, 0]: v_perm_b32 selector c | 0x0c << 8 | (4 + c) << 16 | 0x0c << 24
+          const uint32_t sel = (uint32_t)c | 0x0c00u | ((uint32_t)(4 + c) << 16) | 0x0c000000u;
+          H[c] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(q0, p0, sel)),
+                                        __builtin_bit_cast(u16x2_t, w0), 0u, false) & 0x7fff00u;
+          H[3 + c] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(q1, p1, sel)),
+                                            __builtin_bit_cast(u16x2_t, w1), 0u, false) & 0x7fff00u;
         }
       };
       auto mulhi24 = [](uint32_t x, uint32_t y) -> uint32_t {  // x, y < 2^24: v_mul_hi_u32_u24

@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, 'libffcv_hip.so')
-SOURCES = ['ffcv_common.hip', 'ffcv_rrc.hip', 'ffcv_jpeg.hip', 'ffcv_host.hip']
+SOURCES = ['ffcv_common.hip', 'ffcv_rrc.hip', 'ffcv_jpeg.hip', 'ffcv_host.hip', 'ffcv_cpu_jpeg.hip']
 HEADERS = ['api_internal.h', 'device_common.h']
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950').split(';')[0]
 

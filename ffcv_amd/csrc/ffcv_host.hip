@@ -6,11 +6,11 @@
 //   resize   (libffcv.cpp:33-42)  cv::resize(ROI, dst, INTER_AREA) on host
 //            memory, computed on the CPU by the same single-source INTER_AREA
 //            functions the kernels run (device_common.h ResizePlan ...).
-//   imdecode (libffcv.cpp:53-112) tjDecompress2(TJPF_RGB, TJFLAG_FASTDCT) of
-//            one JPEG in host memory into a host HWC buffer, executed by the
-//            gfx950 JPEG kernels on a per-thread stream and decoder context
-//            (bytes in, pixels out with hipMemcpyAsync).  There is no CPU
-//            JPEG decoder in the product: without a HIP device it returns -1.
+//   ffcv_imdecode_device: imdecode's signature and semantics (libffcv.cpp:
+//            53-112), executed by the gfx950 JPEG kernels on a per-thread
+//            stream and decoder context (bytes in, pixels out with
+//            hipMemcpyAsync).  imdecode itself decodes on the CPU, like the
+//            reference (ffcv_cpu_jpeg.hip).
 //
 // The hot path never comes here: the Loader decodes whole launches on the
 // device (ffcv_jpeg_rrc_fused).  These exist for drop-in compatibility.
@@ -168,9 +168,10 @@ int ffcv_draw_batch_host(const uint64_t *sample_ids, const uint32_t *heights, co
   return FFCV_OK;
 }
 
-int imdecode(unsigned char *input_buffer, uint64_t input_size, uint32_t source_height, uint32_t source_width,
-             unsigned char *output_buffer, uint32_t crop_height, uint32_t crop_width, uint32_t offset_x,
-             uint32_t offset_y, uint32_t scale_num, uint32_t scale_denom, bool enable_crop, bool hflip) {
+int ffcv_imdecode_device(unsigned char *input_buffer, uint64_t input_size, uint32_t source_height,
+                         uint32_t source_width, unsigned char *output_buffer, uint32_t crop_height,
+                         uint32_t crop_width, uint32_t offset_x, uint32_t offset_y, uint32_t scale_num,
+                         uint32_t scale_denom, bool enable_crop, bool hflip) {
   (void)source_height;  // unused by the reference too (libffcv.cpp:53-112)
   (void)source_width;
   (void)offset_x;

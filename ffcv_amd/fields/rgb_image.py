@@ -16,10 +16,11 @@ reference, but the decoders run on the HIP device that the Loader feeds:
 
 A Loader on ``device='cpu'`` runs the reference's own per-sample host loop
 (rgb_image.py:123-136 / 185-210) against the reference-signature C ABI of
-libffcv_hip.so: ``imdecode`` (executed by the gfx950 JPEG kernels, so JPEG
-still needs the HIP device), ``resize`` (INTER_AREA on the CPU, the kernels'
-own functions) and the contract draws (ffcv_draw_batch_host).  Raw-mode
-datasets therefore load on a CPU-only machine; JPEG raises without a GPU.
+libffcv_hip.so: ``imdecode`` (a CPU JPEG decoder with libjpeg-turbo's ifast
++ fancy-upsampling arithmetic, csrc/ffcv_cpu_jpeg.hip, as the reference's
+TurboJPEG call), ``resize`` (INTER_AREA on the CPU, the kernels' own
+functions) and the contract draws (ffcv_draw_batch_host).  Raw and JPEG
+datasets therefore load on a CPU-only machine, as with the reference.
 """
 from abc import ABCMeta, abstractmethod
 from dataclasses import replace

@@ -76,6 +76,8 @@ _SIGS = {
     'resize': (None, [ctypes.c_int64] * 11),
     'imdecode': (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32,
                          c_uint32, c_uint32, c_uint32, c_uint32, ctypes.c_bool, ctypes.c_bool]),
+    'ffcv_imdecode_device': (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32,
+                                     c_uint32, c_uint32, c_uint32, c_uint32, ctypes.c_bool, ctypes.c_bool]),
     'ffcv_host_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int]),
     'ffcv_draw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
@@ -215,15 +217,29 @@ def resize_crop(source, start_row, end_row, start_col, end_col, destination):
 def imdecode(source: np.ndarray, dst: np.ndarray, source_height: int, source_width: int,
              crop_height=None, crop_width=None, offset_x=0, offset_y=0, scale_factor_num=1,
              scale_factor_denom=1, enable_crop=False, do_flip=False):
-    """Decode one JPEG (host bytes) into dst (host HWC uint8), libffcv.py:34-48;
-    runs on the HIP device.  Returns 0 or -1 like tjDecompress2."""
+    """Decode one JPEG (host bytes) into dst (host HWC uint8), libffcv.py:34-48,
+    on the CPU like the reference.  Returns 0 or -1 like tjDecompress2."""
+    return _imdecode(lib().imdecode, source, dst, source_height, source_width, crop_height, crop_width,
+                     offset_x, offset_y, scale_factor_num, scale_factor_denom, enable_crop, do_flip)
+
+
+def imdecode_device(source: np.ndarray, dst: np.ndarray, source_height: int, source_width: int,
+                    crop_height=None, crop_width=None, offset_x=0, offset_y=0, scale_factor_num=1,
+                    scale_factor_denom=1, enable_crop=False, do_flip=False):
+    """imdecode executed by the gfx950 JPEG kernels (host buffers in and out)."""
+    return _imdecode(lib().ffcv_imdecode_device, source, dst, source_height, source_width, crop_height,
+                     crop_width, offset_x, offset_y, scale_factor_num, scale_factor_denom, enable_crop, do_flip)
+
+
+def _imdecode(fn, source, dst, source_height, source_width, crop_height, crop_width, offset_x, offset_y,
+              scale_factor_num, scale_factor_denom, enable_crop, do_flip):
     if crop_height is None:
         crop_height = source_height
     if crop_width is None:
         crop_width = source_width
-    return lib().imdecode(source.ctypes.data, source.size, int(source_height), int(source_width),
-                          dst.ctypes.data, int(crop_height), int(crop_width), int(offset_x), int(offset_y),
-                          int(scale_factor_num), int(scale_factor_denom), bool(enable_crop), bool(do_flip))
+    return fn(source.ctypes.data, source.size, int(source_height), int(source_width),
+              dst.ctypes.data, int(crop_height), int(crop_width), int(offset_x), int(offset_y),
+              int(scale_factor_num), int(scale_factor_denom), bool(enable_crop), bool(do_flip))
 
 
 def host_gather(src: np.ndarray, src_off: np.ndarray, sizes: np.ndarray, dst_off: np.ndarray, dst,

@@ -123,16 +123,29 @@ void resize(int64_t cresizer, int64_t source_p, int64_t sx, int64_t sy,
 
 /* libffcv.cpp:53-112 imdecode (bound at ffcv/libffcv.py:34-48): decode the
  * JPEG input_buffer[input_size] to crop_height x crop_width x 3 RGB in host
- * output_buffer, tjDecompress2(TJPF_RGB, TJFLAG_FASTDCT) semantics, on the
- * HIP device (per-thread stream and decoder context).  Returns 0, or -1 on a
- * decode error / size mismatch / when enable_crop, hflip or a scale other
- * than 1 is requested (never used by ffcv) -- see ffcv_last_error(). */
+ * output_buffer, tjDecompress2(TJPF_RGB, TJFLAG_FASTDCT) semantics (ifast
+ * IDCT, fancy upsampling), on the CPU of the calling thread like the
+ * reference (ffcv_cpu_jpeg.hip; thread-safe, per-thread scratch).  Baseline
+ * / extended sequential Huffman, 8-bit, 1 or 3 components, restart
+ * intervals.  Returns 0, or -1 on a decode error, an unsupported stream
+ * (progressive, arithmetic, multi-scan, CMYK), a size other than the image's,
+ * or when enable_crop, hflip or a scale other than 1 is requested (never
+ * used by ffcv) -- see ffcv_last_error(). */
 int imdecode(unsigned char *input_buffer, uint64_t input_size,
              uint32_t source_height, uint32_t source_width,
              unsigned char *output_buffer, uint32_t crop_height,
              uint32_t crop_width, uint32_t offset_x, uint32_t offset_y,
              uint32_t scale_num, uint32_t scale_denom, bool enable_crop,
              bool hflip);
+
+/* imdecode's signature and semantics, executed by the gfx950 JPEG kernels
+ * (per-thread stream and decoder context; host buffers in and out). */
+int ffcv_imdecode_device(unsigned char *input_buffer, uint64_t input_size,
+                         uint32_t source_height, uint32_t source_width,
+                         unsigned char *output_buffer, uint32_t crop_height,
+                         uint32_t crop_width, uint32_t offset_x,
+                         uint32_t offset_y, uint32_t scale_num,
+                         uint32_t scale_denom, bool enable_crop, bool hflip);
 
 /* Host gather of n byte ranges src + src_off[i] (sizes[i] bytes) to
  * dst + dst_off[i], split over nthreads threads by bytes: the PCIe path's

@@ -1,0 +1,87 @@
+"""imdecode on the CPU (libffcv.cpp:53-112 signature; ffcv_cpu_jpeg.hip)
+against libjpeg-turbo 3.1.4 itself (Pillow-bundled, through the oracle's
+jpeg62 harness with the reference's TurboJPEG settings: ifast IDCT, fancy
+upsampling, RGB out).  No GPU: the reference's CPU Loader decodes here."""
+import io
+import threading
+
+import numpy as np
+from PIL import Image
+
+from ffcv_amd.synthetic import natural_image, encode_jpeg, imagenet_like_shape
+
+
+def _set(rng, n, max_side=300):
+    imgs, blobs = [], []
+    subs = ['4:2:0', '4:2:2', '4:4:4']
+    for k in range(n):
+        if k % 5 == 4:
+            h, w = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        else:
+            h, w = imagenet_like_shape(rng, max_side)
+        img = natural_image(rng, h, w)
+        if k % 11 == 10:
+            img = img[:, :, 0].copy()
+        q = [90, 95, 75, 50, 100, 1, 30][k % 7]
+        blobs.append(encode_jpeg(img, q, subs[k % 3], optimize=k % 4 == 3))
+        imgs.append(img)
+    return imgs, blobs
+
+
+def _pil(img, **kw):
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, 'JPEG', **kw)
+    return np.frombuffer(b.getvalue(), np.uint8).copy()
+
+
+def test_cpu_imdecode_matches_libjpeg_turbo(hip_lib, oracle):
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(41)
+    imgs, blobs = _set(rng, 56)
+    # restart intervals (DRI + RSTn every 1 / 3 MCUs or every MCU row), and
+    # 4:1:1 / 4:4:0 style layouts Pillow writes with explicit factors
+    extra = []
+    for k in range(6):
+        h, w = imagenet_like_shape(rng, 200)
+        img = natural_image(rng, h, w)
+        extra.append((img, _pil(img, quality=85, restart_marker_blocks=[1, 3, 7][k % 3])))
+        extra.append((img, _pil(img, quality=92, restart_marker_rows=1, subsampling=k % 3)))
+    for img, b in extra:
+        imgs.append(img)
+        blobs.append(b)
+    errors = []
+
+    def work(ks):
+        for k in ks:
+            h, w = imgs[k].shape[:2]
+            out = np.zeros((h, w, 3), np.uint8)
+            rc = L.imdecode(blobs[k], out, h, w, h, w, 0, 0, 1, 1, False, False)
+            want = oracle.ljt_decode(blobs[k])
+            if rc != 0 or not np.array_equal(out, want):
+                errors.append((k, rc, int((out != want).sum())))
+    ths = [threading.Thread(target=work, args=(range(t, len(imgs), 4),)) for t in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+
+
+def test_cpu_imdecode_rejects(hip_lib):
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(3)
+    img = natural_image(rng, 40, 56)
+    blob = encode_jpeg(img, 90)
+    out = np.zeros((40, 56, 3), np.uint8)
+    assert L.imdecode(blob, out, 40, 56) == 0
+    bad = blob.copy()
+    bad[:2] = 0  # no SOI
+    assert L.imdecode(bad, out, 40, 56) == -1
+    assert b'SOI' in L.lib().ffcv_last_error()
+    assert L.imdecode(blob, np.zeros((41, 56, 3), np.uint8), 41, 56) == -1  # scaled decode
+    assert L.imdecode(blob, out, 40, 56, enable_crop=True) == -1
+    prog = _pil(img, quality=90, progressive=True)
+    assert L.imdecode(prog, out, 40, 56) == -1
+    assert b'progressive' in L.lib().ffcv_last_error()
+    # truncated stream: decodes (zeros past the end, like libjpeg's warning path), never crashes
+    assert L.imdecode(blob[: len(blob) // 2], out, 40, 56) in (0, -1)

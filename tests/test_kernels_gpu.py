@@ -602,8 +602,8 @@ def test_jpeg_entropy_index(hip_lib, oracle):
 
 
 def test_host_imdecode_matches_libjpeg(hip_lib, oracle):
-    """libffcv.cpp:53-112 imdecode (reference signature, host buffers in and
-    out) executed by the gfx950 kernels: bit-exact with libjpeg-turbo ifast
+    """ffcv_imdecode_device: libffcv.cpp:53-112 imdecode's signature (host
+    buffers in and out) executed by the gfx950 kernels: bit-exact with libjpeg-turbo ifast
     + fancy on mixed subsampling / quality / greyscale / odd sizes, from
     several host threads at once (per-thread stream + decoder context), and
     -1 on a corrupt stream or a size mismatch."""
@@ -619,7 +619,7 @@ def test_host_imdecode_matches_libjpeg(hip_lib, oracle):
         for k in ks:
             h, w = imgs[k].shape[:2]
             out = np.zeros((h, w, 3), np.uint8)
-            rc = L.imdecode(blobs[k], out, h, w, h, w, 0, 0, 1, 1, False, False)
+            rc = L.imdecode_device(blobs[k], out, h, w, h, w, 0, 0, 1, 1, False, False)
             if rc != 0 or not np.array_equal(out, want[k]):
                 errors.append((k, rc))
     ths = [threading.Thread(target=work, args=(range(t, 24, 4),)) for t in range(4)]
@@ -632,8 +632,8 @@ def test_host_imdecode_matches_libjpeg(hip_lib, oracle):
     out = np.zeros((h, w, 3), np.uint8)
     bad = blobs[0].copy()
     bad[:2] = 0  # no SOI
-    assert L.imdecode(bad, out, h, w, h, w) == -1
-    assert L.imdecode(blobs[0], np.zeros((h + 1, w, 3), np.uint8), h + 1, w, h + 1, w) == -1
+    assert L.imdecode_device(bad, out, h, w, h, w) == -1
+    assert L.imdecode_device(blobs[0], np.zeros((h + 1, w, 3), np.uint8), h + 1, w, h + 1, w) == -1
 
 
 def test_jpeg_arena_sizing_and_exhaustion(hip_lib, oracle):

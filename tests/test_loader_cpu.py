@@ -134,15 +134,34 @@ def test_host_draws_match_oracle(oracle):
         assert np.array_equal(crops, oc) and np.array_equal(cut, ocut)
 
 
-def test_cpu_device_jpeg_needs_the_hip_device(tmp_path):
-    """JPEG on device='cpu' decodes through imdecode, which runs on the HIP
-    device: without one it fails loudly (no CPU JPEG decoder in the product)."""
-    if ch.cuda.is_available():
-        pytest.skip('covered by the GPU test of the same path')
-    from ffcv_amd.loader.epoch_iterator import DecodeError
-    fn = write(str(tmp_path / 'j.beton'), NaturalDS(8), {'image': RGBImageField(write_mode='jpg'),
-                                                          'label': IntField()})
-    for pipe in (None, [RandomResizedCropRGBImageDecoder((32, 32)), ToTensor()]):
-        loader = Loader(fn, batch_size=4, device='cpu', pipelines={'image': pipe} if pipe else {})
-        with pytest.raises(DecodeError, match='imdecode'):
-            next(iter(loader))
+def test_cpu_device_loader_jpeg(tmp_path, oracle):
+    """device='cpu' on a JPEG .beton, no GPU involved: the reference's host
+    loop through the reference-signature C ABI -- imdecode on the CPU
+    (ffcv_cpu_jpeg.hip), host draws and INTER_AREA resize -- host tensors
+    out, bit-exact against the oracle (libjpeg-turbo decode + C restatement);
+    and the default Simple pipeline on constant-size JPEGs."""
+    from tests.helpers import samples_of, expected_rrc
+    fn = str(tmp_path / 'cpu_jpg.beton')
+    write(fn, NaturalDS(40, hw=(90, 110), var=True, seed=12),
+          {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    samples = samples_of(fn)
+    loader = Loader(fn, batch_size=8, seed=5, order=OrderOption.RANDOM, device='cpu',
+                    pipelines={'image': [RandomResizedCropRGBImageDecoder((56, 48)), Cutout(7, (9, 8, 7)),
+                                         ToTensor()]})
+    order = np.random.default_rng(5).permutation(40)
+    for b, (images, labels) in enumerate(loader):
+        assert images.device.type == 'cpu'
+        ids = order[b * 8:(b + 1) * 8]
+        want = expected_rrc(oracle, samples, ids, 5, 0, (56, 48), cutout=7, fill=(9, 8, 7), cut_before_flip=True)
+        assert np.array_equal(images.numpy(), want)
+    fn2 = str(tmp_path / 'cpu_jpg_const.beton')
+    write(fn2, NaturalDS(12, hw=(40, 56), seed=13), {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
+    s2 = samples_of(fn2)
+    n = 0
+    for images, labels in Loader(fn2, batch_size=4, device='cpu'):
+        for k in range(4):
+            i = int(np.nonzero([np.array_equal(oracle.ljt_decode(s[0]), images[k].numpy()) for s in s2])[0][0])
+            assert int(labels[k]) == i % 10
+            n += 1
+    assert n == 12
+

@@ -357,33 +357,6 @@ def test_early_break_then_next_epoch(tmpdir_m, oracle):
         assert n == (5 if epoch == 1 else 10)
 
 
-def test_cpu_device_loader_jpeg(tmpdir_m, oracle):
-    """device='cpu' on a JPEG .beton: the reference's host loop through the
-    reference-signature C ABI (imdecode on the HIP device, host draws and
-    INTER_AREA resize), host tensors out, bit-exact against the oracle; and
-    the default Simple pipeline on constant-size JPEGs."""
-    fn = os.path.join(tmpdir_m, 'cpu_jpg.beton')
-    write(fn, NaturalDS(40, hw=(90, 110), var=True, seed=12),
-          {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
-    samples = _samples(fn)
-    loader = Loader(fn, batch_size=8, seed=5, order=OrderOption.RANDOM, device='cpu',
-                    pipelines={'image': [RandomResizedCropRGBImageDecoder((56, 48)), Cutout(7, (9, 8, 7)),
-                                         ToTensor()]})
-    order = np.random.default_rng(5).permutation(40)
-    for b, (images, labels) in enumerate(loader):
-        assert images.device.type == 'cpu'
-        ids = order[b * 8:(b + 1) * 8]
-        want = _expected(oracle, samples, ids, 5, 0, (56, 48), cutout=7, fill=(9, 8, 7), cut_before_flip=True)
-        assert np.array_equal(images.numpy(), want)
-    fn2 = os.path.join(tmpdir_m, 'cpu_jpg_const.beton')
-    write(fn2, NaturalDS(12, hw=(40, 56), seed=13), {'image': RGBImageField(write_mode='jpg'), 'label': IntField()})
-    s2 = _samples(fn2)
-    for images, labels in Loader(fn2, batch_size=4, device='cpu'):
-        for k in range(4):
-            i = int(np.nonzero([np.array_equal(oracle.jpeg_decode(s[0]), images[k].numpy()) for s in s2])[0][0])
-            assert int(labels[k]) == i % 10
-
-
 def test_entropy_index_epochs_match(tmpdir_m, oracle):
     """The entropy index (default on with device_cache) changes no output:
     three epochs with it equal three epochs without it, every sample's record

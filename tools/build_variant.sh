@@ -6,4 +6,4 @@ NAME=$1; shift
 mkdir -p build/ab
 cd ffcv_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off -fno-fast-math \
-  -Wno-unused-function "$@" -o ../../build/ab/$NAME.so ffcv_common.hip ffcv_rrc.hip ffcv_jpeg.hip ffcv_host.hip
+  -Wno-unused-function "$@" -o ../../build/ab/$NAME.so ffcv_common.hip ffcv_rrc.hip ffcv_jpeg.hip ffcv_host.hip ffcv_cpu_jpeg.hip

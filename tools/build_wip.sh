@@ -11,5 +11,5 @@ cp ffcv_amd/csrc/* $TMP/a/b/
 cp $SRC $TMP/a/b/ffcv_jpeg.hip
 mkdir -p build/ab
 (cd $TMP/a/b && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off -fno-fast-math \
-  -Wno-unused-function -I$OLDPWD/include "$@" -o $OLDPWD/build/ab/$NAME.so ffcv_common.hip ffcv_rrc.hip ffcv_jpeg.hip ffcv_host.hip)
+  -Wno-unused-function -I$OLDPWD/include "$@" -o $OLDPWD/build/ab/$NAME.so ffcv_common.hip ffcv_rrc.hip ffcv_jpeg.hip ffcv_host.hip ffcv_cpu_jpeg.hip)
 rm -rf $TMP

@@ -245,25 +245,29 @@ def parity_check(cfg, slots, order, batch, tile, offs, sizes, hs, ws, rows_total
                     'required, checked after the timed region'}
 
 
-def c5_subresult(timeout_s=150):
-    """BASELINE configs[4] (C5, "the HBM-bound roofline point": raw 512x512
-    RGB, RRC 448 + Cutout 64, batch 256) measured beside the headline, never
-    as `value`: this script in a child process with --config c5 (1,024
-    unique raw encodings replicated to the 10,000-sample .beton, 200 timed
-    steps, parity-checked); its line is returned with its own roofline."""
+def sub_result(config, timeout_s=150):
+    """The other device-resident BASELINE configs measured beside the
+    headline, never as `value` (BASELINE.md "device-resident img/s for C2, C3
+    and C5"): this script in a child process with --config c5 (C5, "the
+    HBM-bound roofline point": raw 512x512 RGB, RRC 448 + Cutout 64, batch
+    256; 1,024 unique raw encodings replicated to the 10,000-sample .beton)
+    or --config c2 (C2: 10k-JPEG .beton, RRC 224 u8, batch 256; 10,000
+    unique encodings), 200 timed steps, parity-checked; its line is returned
+    with its own roofline."""
     import subprocess
-    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', 'c5', '--steps', '200', '--warmup', '20',
-           '--unique', '1024', '--no-cpu-baseline', '--parity-rows', '512']
+    unique = {'c5': '1024', 'c2': '10000'}[config]
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', config, '--steps', '200', '--warmup', '20',
+           '--unique', unique, '--no-cpu-baseline', '--no-later-epochs', '--parity-rows', '512']
     env = dict(os.environ)
     for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
         env.pop(k, None)
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
     except subprocess.TimeoutExpired:
-        return {'error': f'c5 run exceeded {timeout_s}s'}
+        return {'error': f'{config} run exceeded {timeout_s}s'}
     lines = [l for l in r.stdout.strip().splitlines() if l.startswith('{')]
     if r.returncode != 0 or not lines:
-        return {'error': f'c5 run failed (rc {r.returncode}): {r.stderr.strip()[-400:]}'}
+        return {'error': f'{config} run failed (rc {r.returncode}): {r.stderr.strip()[-400:]}'}
     d = json.loads(lines[-1])
     keep = ('metric', 'value', 'unit', 'steps', 'warmup', 'ms_per_step', 'dtype', 'data', 'config', 'roofline',
             'parity')
@@ -286,7 +290,7 @@ def main():
     ap.add_argument('--steps', type=int, default=400)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='c3', choices=list(CONFIGS))
-    ap.add_argument('--unique', type=int, default=16384,
+    ap.add_argument('--unique', type=int, default=65536,
                     help='unique synthetic encodings replicated over the dataset (generated once per box, /tmp cache)')
     ap.add_argument('--dataset-size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -311,7 +315,7 @@ def main():
     ap.add_argument('--no-later-epochs', action='store_true',
                     help='skip the later-epoch (entropy index) measurement reported beside the headline')
     ap.add_argument('--no-c5', action='store_true',
-                    help='skip the C5 (raw, HBM-bound) sub-result the default C3 run reports beside its value')
+                    help='skip the C5 (raw, HBM-bound) and C2 sub-results the default C3 run reports beside its value')
     ap.add_argument('--no-kernel-events', action='store_true',
                     help='do not record HIP events around each kernel of the timed launches (per-kernel roofline)')
     ap.add_argument('--parity-rows', type=int, default=1536,
@@ -830,7 +834,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(args.config, tile, offs, sizes, hs, ws, args.cpu_budget)
     if rank == 0 and world == 1 and args.config == 'c3' and not args.no_c5 and not (args.only or args.k2flags):
-        res['c5'] = c5_subresult()
+        res['c5'] = sub_result('c5')
+        res['c2'] = sub_result('c2')
     if rank == 0:
         print(json.dumps(res, default=lambda o: o.item() if hasattr(o, 'item') else str(o)), flush=True)
     if dist:

@@ -19,7 +19,9 @@
 // Requests whose size differs from the image's (TurboJPEG's scaled decode)
 // and the tjTransform crop / flip (enable_crop, hflip) are not supported
 // either: ffcv passes the image's own size and False, False, 1, 1.
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "api_internal.h"
@@ -216,6 +218,20 @@ struct Bits {
   int n = 0;
   bool marker = false;
   void fill() {
+    // fast path: 8 bytes with no 0xFF among them enter whole
+    if (!marker && end - p >= 8) {
+      uint64_t v;
+      std::memcpy(&v, p, 8);
+      const uint64_t x = ~v;  // a 0xFF byte of v is a zero byte of x
+      if (!((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull)) {
+        v = __builtin_bswap64(v);
+        const int k = (64 - n) >> 3;  // whole bytes that fit
+        acc |= (k == 8 ? v : v >> (64 - 8 * k)) << (64 - n - 8 * k);
+        n += 8 * k;
+        p += k;
+        return;
+      }
+    }
     while (n <= 56) {
       int v = 0;
       if (!marker && p < end) {
@@ -488,14 +504,20 @@ void upsample_row(const Dec &d, int ci, const uint8_t *pl, int stride, int y, in
       for (int x = 0; x < W; x++) out[x] = pl[(size_t)row * stride + (x >> 1)];
       return;
     }
-    auto cs = [&](int col) { return a[col] * 3 + o[col]; };
-    for (int x = 0; x < W; x++) {
-      const int col = x >> 1, t = cs(col);
-      if (x & 1)
-        out[x] = (t * 3 + (col + 1 < cw ? cs(col + 1) : t) + 7) >> 4;
-      else
-        out[x] = (t * 3 + (col > 0 ? cs(col - 1) : t) + 8) >> 4;
+    // h2v2_fancy_upsample: column sums of the row and its context row, then
+    // the 3:1 horizontal triangle with the edge columns replicated
+    thread_local std::vector<int> cs;
+    cs.resize((size_t)cw + 2);
+    int *c = cs.data() + 1;
+    for (int col = 0; col < cw; col++) c[col] = a[col] * 3 + o[col];
+    c[-1] = c[0];
+    c[cw] = c[cw - 1];
+    for (int x = 0; x + 1 < W; x += 2) {
+      const int col = x >> 1, t = c[col] * 3;
+      out[x] = (t + c[col - 1] + 8) >> 4;
+      out[x + 1] = (t + c[col + 1] + 7) >> 4;
     }
+    if (W & 1) out[W - 1] = (c[(W - 1) >> 1] * 3 + c[((W - 1) >> 1) - 1] + 8) >> 4;
   } else {  // int_upsample
     const uint8_t *r = pl + (size_t)(y / ve) * stride;
     for (int x = 0; x < W; x++) out[x] = r[x / he];
@@ -565,6 +587,64 @@ int imdecode(unsigned char *input_buffer, uint64_t input_size, uint32_t source_h
     }
   }
   return 0;
+}
+
+// The reference's per-sample CPU loop under numba prange (rgb_image.py:
+// 123-136 Simple, :185-210 ResizedCrop) as one native call over nthreads
+// threads: sample k (bytes data[k][0, sizes[k]), h x w, mode 0 = jpg, 1 =
+// raw, anything else = skip) is decoded by imdecode or taken as is, then
+// with crops (B x 4: i, j, h, w) cut and resized by resize() (INTER_AREA) to
+// out_h x out_w, or without crops written whole, at out + k * out_stride.
+// status[k] = 0, or -1 when its decode failed (ffcv_last_error() holds the
+// last message).  Samples are handed out one at a time from an atomic
+// counter (their sizes differ).
+int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes, const uint32_t *heights,
+                          const uint32_t *widths, const uint32_t *modes, int batch, const int32_t *crops,
+                          int out_h, int out_w, uint8_t *out, uint64_t out_stride, int nthreads,
+                          int32_t *status) {
+  if (batch < 0 || (batch > 0 && (!data || !sizes || !heights || !widths || !modes || !out || !status)) ||
+      (crops && (out_h <= 0 || out_w <= 0))) {
+    ffcv::set_error("ffcv_cpu_decode_batch: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    std::vector<uint8_t> img;
+    for (int k = next.fetch_add(1); k < batch; k = next.fetch_add(1)) {
+      const uint32_t h = heights[k], w = widths[k], mode = modes[k];
+      status[k] = 0;
+      if (mode > 1) continue;
+      uint8_t *dst = out + (uint64_t)k * out_stride;
+      const uint8_t *src = data[k];
+      if (mode == 0) {
+        uint8_t *o = dst;
+        if (crops) {
+          img.resize((size_t)h * w * 3);
+          o = img.data();
+        }
+        if (imdecode(const_cast<uint8_t *>(data[k]), sizes[k], h, w, o, h, w, 0, 0, 1, 1, false, false) != 0) {
+          status[k] = -1;
+          continue;
+        }
+        src = o;
+      } else if (!crops) {
+        std::memcpy(dst, src, (size_t)h * w * 3);
+        continue;
+      }
+      if (crops) {
+        const int32_t *c = crops + 4 * k;
+        resize(0, (int64_t)(uintptr_t)src, h, w, c[0], c[0] + c[2], c[1], c[1] + c[3], (int64_t)(uintptr_t)dst,
+               out_h, out_w);
+      }
+    }
+  };
+  const int T = std::max(1, std::min(nthreads, batch));
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; t++) th.emplace_back(work);
+  work();
+  for (auto &x : th) x.join();
+  return FFCV_OK;
 }
 
 }  // extern "C"

@@ -128,6 +128,50 @@ void resize(int64_t cresizer, int64_t source_p, int64_t sx, int64_t sy, int64_t 
   HostPlan h;
   make_host_plan(h, (int)sw, (int)sh, (int)ty, (int)tx);
   const ResizePlan &P = h.P;
+  if (P.kind == 3) {
+    // resize.cpp's separable form of resize_linear: HResizeLinear once per
+    // source row into an int row (two rows cached, as the kernels' walk),
+    // then VResizeLinear per element -- the SSE2 body's (sat_s16(h >> 4) *
+    // c) >> 16 sums below vec_end, the scalar tail's rounding after it.
+    const int dw = (int)ty, dh = (int)tx, n = dw * 3;
+    thread_local std::vector<int> hbuf;
+    hbuf.resize((size_t)2 * n);
+    int *HA = hbuf.data(), *HB = HA + n;
+    int ca = -1, cb = -1;
+    auto hrow = [&](int r, int *H) {
+      const uint8_t *rp = S.p + (uint64_t)r * S.step;
+      for (int dx = 0; dx < dw; dx++) {
+        const LinTap &l = h.lx[dx];
+        const uint8_t *q = rp + (uint64_t)l.s * 3;
+        for (int c = 0; c < 3; c++) H[dx * 3 + c] = l.border ? q[c] * 2048 : q[c] * l.c0 + q[c + 3] * l.c1;
+      }
+    };
+    for (int dy = 0; dy < dh; dy++) {
+      const LinTap &ly = h.ly[dy];
+      const int ra = std::min(std::max(ly.s, 0), P.sh - 1), rb = std::min(std::max(ly.s + 1, 0), P.sh - 1);
+      if (ra != ca) {
+        if (ra == cb) {
+          std::swap(HA, HB);
+          std::swap(ca, cb);
+        } else {
+          hrow(ra, HA);
+          ca = ra;
+        }
+      }
+      if (rb != cb) {
+        hrow(rb, HB);
+        cb = rb;
+      }
+      uint8_t *row = dst + (uint64_t)dy * n;
+      const int ve = std::min(P.vec_end, n);
+      for (int e = 0; e < ve; e++) {
+        const int m0 = (sat_s16i(HA[e] >> 4) * ly.c0) >> 16, m1 = (sat_s16i(HB[e] >> 4) * ly.c1) >> 16;
+        row[e] = (uint8_t)sat_u8i((sat_s16i(m0 + m1) + 2) >> 2);
+      }
+      for (int e = ve; e < n; e++) row[e] = (uint8_t)sat_u8i((HA[e] * ly.c0 + HB[e] * ly.c1 + (1 << 21)) >> 22);
+    }
+    return;
+  }
   for (int dy = 0; dy < (int)tx; dy++) {
     uint8_t *row = dst + (uint64_t)dy * ty * 3;
     for (int dx = 0; dx < (int)ty; dx++) {

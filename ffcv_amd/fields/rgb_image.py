@@ -66,12 +66,17 @@ def _pipeline_device(op):
     return getattr(op, '_pipeline_device', None) or ch.device('cpu')
 
 
-def _host_imdecode(L, data, out, h, w):
-    """libffcv imdecode of one sample into a host buffer; raises on failure
-    (the reference ignores the status, rgb_image.py:131,196)."""
-    if L.imdecode(data, out, h, w, h, w, 0, 0, 1, 1, False, False) != 0:
+def _host_threads():
+    from ..pipeline.compiler import Compiler
+    return max(1, int(Compiler.num_threads))
+
+
+def _raise_failed(L, status, ids):
+    bad = np.nonzero(status != 0)[0]
+    if bad.size:
         from ..loader.epoch_iterator import DecodeError
-        raise DecodeError('imdecode failed: ' + L.lib().ffcv_last_error().decode(errors='replace'))
+        raise DecodeError(f'imdecode failed for sample {int(ids[bad[0]])}: '
+                          + L.lib().ffcv_last_error().decode(errors='replace'))
 
 
 class SimpleRGBImageDecoder(Operation):
@@ -139,14 +144,18 @@ instead."""
                     todo = np.nonzero(~raw)[0]
                 else:
                     todo = range(B)
-                for dst_ix in todo:
-                    field = fields[dst_ix]
-                    image_data = mem_read(field['data_ptr'], storage_state)
-                    if field['mode'] == IMAGE_MODES['jpg']:
-                        _host_imdecode(L, image_data, destination[dst_ix], int(field['height']),
-                                       int(field['width']))
-                    else:
-                        L.memcpy(image_data, destination[dst_ix])
+                todo = np.asarray(todo, np.int64)
+                if todo.size:
+                    # the remaining samples (JPEG, or raw the gather did not take)
+                    # through one native call over the Loader's threads
+                    take = set(todo.tolist())
+                    images = [mem_read(fields[k]['data_ptr'], storage_state) if k in take else None
+                              for k in range(B)]
+                    modes = np.full(B, 2, np.uint32)  # 2: skip (gathered above)
+                    modes[todo] = np.where(fields['mode'][todo] == IMAGE_MODES['jpg'], 0, 1)
+                    status = L.cpu_decode_batch(images, fields['height'], fields['width'], modes, destination[:B],
+                                                nthreads=_host_threads())
+                    _raise_failed(L, status, np.asarray(batch_indices))
                 return destination[:B]
             return decode_host
 
@@ -261,19 +270,15 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
             dp = self._make_draw_params_seed(seed, epoch, out_h, out_w)
             crops = np.empty((B, 4), np.int32)
             L.draw_batch_host(ids, fields['height'], fields['width'], dp, crops)
-            for k in range(B):
-                field = fields[k]
-                h, w = int(field['height']), int(field['width'])
-                image_data = mem_read(field['data_ptr'], storage_state)
-                if field['mode'] == jpg:
-                    buf = temp_storage[k][:h * w * 3]
-                    _host_imdecode(L, image_data, buf, h, w)
-                    img = buf.reshape(h, w, 3)
-                else:
-                    img = image_data.reshape(h, w, 3)
-                i, j, ch_, cw = (int(x) for x in crops[k])
-                L.resize_crop(img, i, i + ch_, j, j + cw, destination[k])
-            return destination[:B]
+            # imdecode -> crop -> resize per sample, the reference's prange loop
+            # (rgb_image.py:185-210) as one native call over the Loader's threads
+            images = [mem_read(f['data_ptr'], storage_state) for f in fields]
+            modes = np.where(fields['mode'] == jpg, 0, 1)
+            dst = destination[:B]
+            status = L.cpu_decode_batch(images, fields['height'], fields['width'], modes, dst, crops,
+                                        nthreads=_host_threads())
+            _raise_failed(L, status, ids)
+            return dst
         decode.is_parallel = True
         return decode
 

@@ -76,6 +76,8 @@ _SIGS = {
     'resize': (None, [ctypes.c_int64] * 11),
     'imdecode': (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32,
                          c_uint32, c_uint32, c_uint32, c_uint32, ctypes.c_bool, ctypes.c_bool]),
+    'ffcv_cpu_decode_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                      c_int, c_void_p, c_uint64, c_int, c_void_p]),
     'ffcv_imdecode_device': (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32,
                                      c_uint32, c_uint32, c_uint32, c_uint32, ctypes.c_bool, ctypes.c_bool]),
     'ffcv_host_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int]),
@@ -240,6 +242,35 @@ def _imdecode(fn, source, dst, source_height, source_width, crop_height, crop_wi
     return fn(source.ctypes.data, source.size, int(source_height), int(source_width),
               dst.ctypes.data, int(crop_height), int(crop_width), int(offset_x), int(offset_y),
               int(scale_factor_num), int(scale_factor_denom), bool(enable_crop), bool(do_flip))
+
+
+def cpu_decode_batch(images, heights, widths, modes, out: np.ndarray, crops=None, nthreads=1):
+    """The reference's per-sample CPU decode loop as one native call
+    (ffcv_cpu_decode_batch): images[k] are host uint8 arrays (JPEG bytes or
+    raw HWC pixels), out is [B, ...] C-contiguous uint8 (the sample's whole
+    image, or its crops[k] resized to out.shape[1:3]).  Returns the status
+    array (0 / -1 per sample)."""
+    B = len(images)
+    ptrs = np.array([im.ctypes.data if im is not None else 0 for im in images], np.uint64)
+    sizes = np.array([im.size if im is not None else 0 for im in images], np.uint64)
+    hs = np.ascontiguousarray(heights, np.uint32)
+    ws = np.ascontiguousarray(widths, np.uint32)
+    ms = np.ascontiguousarray(modes, np.uint32)
+    status = np.zeros(B, np.int32)
+    if not out.flags['C_CONTIGUOUS'] or out.dtype != np.uint8:
+        raise ValueError('cpu_decode_batch: out must be C-contiguous uint8')
+    stride = out[0].nbytes if B else 0
+    cr = None
+    oh = ow = 0
+    if crops is not None:
+        cr = np.ascontiguousarray(crops, np.int32)
+        oh, ow = int(out.shape[1]), int(out.shape[2])
+    rc = lib().ffcv_cpu_decode_batch(ptrs.ctypes.data, sizes.ctypes.data, hs.ctypes.data, ws.ctypes.data,
+                                     ms.ctypes.data, B, cr.ctypes.data if cr is not None else None, oh, ow,
+                                     out.ctypes.data, stride, int(max(1, nthreads)), status.ctypes.data)
+    if rc != 0:
+        raise RuntimeError('ffcv_cpu_decode_batch: ' + lib().ffcv_last_error().decode(errors='replace'))
+    return status
 
 
 def host_gather(src: np.ndarray, src_off: np.ndarray, sizes: np.ndarray, dst_off: np.ndarray, dst,

@@ -138,6 +138,19 @@ int imdecode(unsigned char *input_buffer, uint64_t input_size,
              uint32_t scale_num, uint32_t scale_denom, bool enable_crop,
              bool hflip);
 
+/* The reference's per-sample CPU decode loop (rgb_image.py:123-136 Simple,
+ * :185-210 ResizedCrop, under numba prange) as one call over nthreads host
+ * threads: sample k (data[k], sizes[k] bytes, heights[k] x widths[k], modes[k]
+ * 0 = jpg through imdecode, 1 = raw, other = skipped) is written whole at
+ * out + k * out_stride, or, with crops (batch x 4: i, j, h, w), cut and resized
+ * by resize() to out_h x out_w there.  status[k] = 0, or -1 when its decode
+ * failed.  Returns FFCV_OK or FFCV_EINVAL. */
+int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes,
+                          const uint32_t *heights, const uint32_t *widths,
+                          const uint32_t *modes, int batch, const int32_t *crops,
+                          int out_h, int out_w, uint8_t *out, uint64_t out_stride,
+                          int nthreads, int32_t *status);
+
 /* imdecode's signature and semantics, executed by the gfx950 JPEG kernels
  * (per-thread stream and decoder context; host buffers in and out). */
 int ffcv_imdecode_device(unsigned char *input_buffer, uint64_t input_size,

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
                    void *__restrict__ out) {
   __shared__ uint16_t s_lut[FP16 ? 768 : 1];
   __shared__ uint4 s_src[RRC_LDS_BYTES / 16];
-  __shared__ LinTap s_rt[RRC_BAND];
+  __shared__ uint4 s_rt[RRC_BAND];  // linear row taps: {ra, rb, c0 << 8, c1 << 8}
   __shared__ AreaTaps s_at[RRC_BAND];
   const int k = blockIdx.y;
   const int t = threadIdx.x;
@@ -174,7 +174,11 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
         if (dst[j] >= 0) s_src[dst[j]] = v[j];
     }
   }
-  if (P.kind == 3 && t < oy1 - oy0) s_rt[t] = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+  if (P.kind == 3 && t < oy1 - oy0) {  // clamped source rows, weights << 8: no per-row clamps in the walk
+    const LinTap l = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+    s_rt[t] = make_uint4((uint32_t)min(max(l.s, 0), P.sh - 1), (uint32_t)min(max(l.s + 1, 0), P.sh - 1),
+                         ((uint32_t)l.c0 & 0xfffu) << 8, ((uint32_t)l.c1 & 0xfffu) << 8);
+  }
   if (P.kind == 2 && t < oy1 - oy0) s_at[t] = area_taps(P.sh, P.scale_y, oy0 + t);
   __syncthreads();
 
@@ -391,8 +395,8 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
     int ca = -1, cb = -1;
     uint32_t HA[12], HB[12];
     for (int dy = gy0; dy < gy1; dy++) {
-      const LinTap ly = s_rt[dy - oy0];
-      const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
+      const uint4 ly = s_rt[dy - oy0];
+      const int ra = (int)ly.x, rb = (int)ly.y;
       if (ra != ca) {
         if (ra == cb) {
 #pragma unroll
@@ -406,7 +410,7 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
         hrow(rb, HB);
         cb = rb;
       }
-      const uint32_t c0 = ((uint32_t)ly.c0 & 0xfffu) << 8, c1 = ((uint32_t)ly.c1 & 0xfffu) << 8;
+      const uint32_t c0 = ly.z, c1 = ly.w;
       int v[12];
 #pragma unroll
       for (int i = 0; i < 12; i++)  // VResizeLinearVec_32s8u: (m0 + 2 + m1) >> 2, no saturation (see hrow)

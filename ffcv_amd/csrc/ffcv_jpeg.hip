@@ -2544,7 +2544,10 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       // once; a row tests its own range)
       const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
       const int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
-      const int ya = oy0 + sub * half, yb = (a.k2flags & 512) ? ya : min(oy1, ya + half);
+      // (a row group is two whole waves: its rows are wave-uniform, so the
+      // per-row tap read, cutout test and row changes are scalar)
+      const int ya = __builtin_amdgcn_readfirstlane(oy0 + sub * half);
+      const int yb = __builtin_amdgcn_readfirstlane((a.k2flags & 512) ? ya : min(oy1, ya + half));
       int ca = -1, cb = -1;
       uint32_t HA[6], HB[6];
       for (int dy = ya; dy < yb; dy++) {

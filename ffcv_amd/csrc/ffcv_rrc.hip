@@ -308,7 +308,10 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
     const int groups = RRC_THREADS / tpg;
     const int per = (oy1 - oy0 + groups - 1) / groups;
     const int g = t / tpg, q = t - g * tpg;
-    const int gy0 = oy0 + g * per, gy1 = min(oy1, gy0 + per);
+    // (a row group is whole waves, tpg >= 64: its rows are wave-uniform, so
+    // the per-row cutout range test is scalar)
+    const int gy0 = __builtin_amdgcn_readfirstlane(oy0 + g * per);
+    const int gy1 = __builtin_amdgcn_readfirstlane(min(oy1, gy0 + per));
     if (q >= nq || gy0 >= gy1) return;
     const int dx0 = 4 * q;
     // cutout: the columns of this thread's quad inside the square (bit j =

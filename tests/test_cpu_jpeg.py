@@ -85,3 +85,44 @@ def test_cpu_imdecode_rejects(hip_lib):
     assert b'progressive' in L.lib().ffcv_last_error()
     # truncated stream: decodes (zeros past the end, like libjpeg's warning path), never crashes
     assert L.imdecode(blob[: len(blob) // 2], out, 40, 56) in (0, -1)
+
+
+def test_cpu_decode_batch(hip_lib, oracle):
+    """ffcv_cpu_decode_batch: the per-sample CPU loop as one threaded call --
+    JPEG and raw samples, whole images and crops resized by INTER_AREA, a
+    skipped sample, and a corrupt one reported in its status only."""
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(7)
+    imgs = [natural_image(rng, int(rng.integers(40, 120)), int(rng.integers(40, 120))) for _ in range(12)]
+    blobs = [encode_jpeg(im, 90, ['4:2:0', '4:4:4'][k % 2]) for k, im in enumerate(imgs)]
+    modes = np.array([0, 1] * 6, np.uint32)
+    srcs = [blobs[k] if modes[k] == 0 else imgs[k].reshape(-1) for k in range(12)]
+    hs = np.array([im.shape[0] for im in imgs], np.uint32)
+    ws = np.array([im.shape[1] for im in imgs], np.uint32)
+    decoded = [oracle.ljt_decode(blobs[k]) if modes[k] == 0 else imgs[k] for k in range(12)]
+    # crops resized to 32 x 48
+    crops = np.array([[k % 5, k % 7, int(hs[k]) // 2, int(ws[k]) // 2] for k in range(12)], np.int32)
+    out = np.zeros((12, 32, 48, 3), np.uint8)
+    st = L.cpu_decode_batch(srcs, hs, ws, modes, out, crops, nthreads=4)
+    assert (st == 0).all()
+    for k in range(12):
+        i, j, h, w = crops[k]
+        want = oracle.resize_crop(decoded[k], i, i + h, j, j + w, 32, 48)
+        assert np.array_equal(out[k], want), k
+    # whole images (the Simple decoder): a fixed-size destination per sample
+    H, W = int(hs.max()), int(ws.max())
+    full = np.zeros((12, H, W, 3), np.uint8)
+    modes2 = modes.copy()
+    modes2[3] = 2  # skipped: left untouched
+    bad = [s.copy() for s in srcs]
+    bad[4] = bad[4].copy()
+    bad[4][:2] = 0  # corrupt JPEG
+    st = L.cpu_decode_batch(bad, hs, ws, modes2, full, nthreads=3)
+    assert st[4] == -1 and (np.delete(st, 4) == 0).all()
+    for k in range(12):
+        if k in (3, 4):
+            continue
+        h, w = int(hs[k]), int(ws[k])
+        got = full[k].reshape(-1)[:h * w * 3].reshape(h, w, 3)
+        assert np.array_equal(got, decoded[k]), k
+    assert not full[3].any()

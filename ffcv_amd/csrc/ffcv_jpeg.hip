@@ -97,7 +97,7 @@
 #endif
 #define K2_COLS 128  // K2 fast path: output column-pair slots (out_w <= 256); K2T / K2_COLS row groups
 #ifndef K2_LDS
-#define K2_LDS 24576  // K2 dynamic LDS: 6 workgroups per CU; bigger bands take the general path (32 KB measured 3% slower)
+#define K2_LDS 26624  // K2 dynamic LDS: the most that keeps 6 workgroups per CU (6 x 26 KB of 160 KB; 512 B granules); bigger bands take the general path (24 KB: 1% slower at C3, 32 KB: 3% slower)
 #endif
 #ifndef JW
 #define JW 4  // waves per K1 workgroup

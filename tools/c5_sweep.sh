@@ -5,10 +5,10 @@
 set -e
 mkdir -p gpurun_out
 for v in ${VARIANTS:-default}; do
-  lib=""; [ "$v" != default ] && lib=$PWD/build/ab/$v.so
+  lib=""; libarg=""; [ "$v" != default ] && lib=$PWD/build/ab/$v.so && libarg="--lib $lib"
   FFCV_HIP_LIB=$lib timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
     tests/test_kernels_gpu.py -k raw_rrc > gpurun_out/c5sw_t_$v.log 2>&1
   echo "$v tests: $(tail -1 gpurun_out/c5sw_t_$v.log)"
-  timeout -k 10 200 python bench.py --lib $lib --config c5 --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/c5sw_$v.log 2>&1
-  python -c "import json;d=json.loads(open('gpurun_out/c5sw_$v.log').read().strip().splitlines()[-1]);print('$v', d['value'], 'img/s', d['roofline']['kernel_ms'], 'ms/launch')"
+  timeout -k 10 200 python bench.py $libarg --config c5 --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/c5sw_$v.log 2>&1
+  python -c "import json;d=json.loads(open('gpurun_out/c5sw_$v.log').read().strip().splitlines()[-1]);print('$v', d['value'], 'img/s', d['roofline']['launch_ms'], 'ms/launch', d['roofline']['frac'])"
 done

@@ -2377,13 +2377,15 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       TPlane tp[3];
       // tile staging: the first SU dwords per thread of every component are
       // loaded before any LDS write (one memory round trip, not one per
-      // dword); row = i / wpr by a float reciprocal (exact: i < 2^11 here)
+      // dword); row = i / wpr by a float reciprocal: exact while the +0.5
+      // margin, 0.5 / (i + 0.5) relative, exceeds v_rcp_f32's 1 ulp plus the
+      // product's rounding (i < 2^20; tiles here hold < 2^13 dwords)
       constexpr int SU = 4;
       uint32_t sv[3][SU];
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         const int wpr = max(tpitch[c] >> 2, 1), n = (a.k2flags & 1024) ? 0 : trows[c] * (tpitch[c] >> 2);
-        const float rwp = 1.0f / (float)wpr;
+        const float rwp = __builtin_amdgcn_rcpf((float)wpr);  // (1 ulp: far inside the +0.5 margin)
         const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
 #pragma unroll
         for (int u = 0; u < SU; u++) {
@@ -2400,8 +2402,9 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
         for (int u = 0; u < SU; u++)
           if (u * K2T + t < n) tl[u * K2T + t] = sv[c][u];
         const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
+        const float rwp = __builtin_amdgcn_rcpf((float)wpr);
         for (int i = SU * K2T + t; i < n; i += K2T) {  // big tiles
-          const int rr = i / wpr, q = i - rr * wpr;
+          const int rr = (int)(((float)i + 0.5f) * rwp), q = i - __mul24(rr, wpr);
           tl[i] = *(const uint32_t *)(src + (uint64_t)rr * gp[c].stride + 4 * q);
         }
         tp[c] = TPlane{(const uint8_t *)tl, ty0[c], tx0[c], tpitch[c]};
@@ -2421,7 +2424,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
         const int R0 = Y0 >> 1, R1 = Y1 >> 1, C0 = X0 >> 1, C1 = X1 >> 1;
         const int npairs = (C1 - C0 + 2) >> 1;
         const int ps = min(npairs, K2T);  // pairs per sweep of the workgroup
-        const float rp = 1.0f / (float)ps;
+        const float rp = __builtin_amdgcn_rcpf((float)ps);
         // ng row groups; t = g * ps + pair (quotients by a float reciprocal:
         // exact for these small operands, as in the tile staging)
         const int ng = (int)(((float)K2T + 0.5f) * rp);

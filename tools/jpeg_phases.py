@@ -55,3 +55,13 @@ print('rounds hist', np.bincount(d[:, 12].astype(int))[:20], 'nthr mean', d[:, 1
 st = (d[:, 0] - d[:, 0].min()) / 100.0
 print('start offsets us: p50', np.median(st), 'max', st.max())
 print('sync wave-iterations mean', d[:, 14].mean(), 'max', d[:, 14].max(), '| write wave-iterations mean', d[:, 15].mean(), 'max', d[:, 15].max())
+# workgroup hold: a K1 workgroup (JW images, one per wave) keeps its LDS until
+# its slowest image is done; idle = the other waves' time between their own
+# end and the workgroup's end
+JW = int(os.environ.get('JW', '4'))
+n = (B // JW) * JW
+s0 = d[:n, 0].reshape(-1, JW).astype(np.float64); e = d[:n, 9].reshape(-1, JW).astype(np.float64)
+wg_end = e.max(1, keepdims=True); wg_start = s0.min(1, keepdims=True)
+busy = (e - s0).sum(); held = (wg_end - s0).sum()
+print(f'workgroup hold: busy wave-time {busy / 100:.0f} us, held {held / 100:.0f} us, idle fraction {1 - busy / held:.3f}')
+print(f'per-image busy us: mean {((e - s0) / 100).mean():.1f} cv {((e - s0).std() / (e - s0).mean()):.3f}')

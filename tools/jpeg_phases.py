@@ -17,7 +17,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 tile, offs, sizes, hs, ws = make_unique('jpg', 256, 4096, 0, 16)
 dev = torch.device('cuda:0')
 d_data = torch.from_numpy(tile).to(dev)
-idx = np.random.default_rng(1).permutation(len(offs))[:B]
+idx = np.resize(np.random.default_rng(1).permutation(len(offs)), B)  # (repeats past the unique count)
 smp = np.zeros(B, L.SAMPLE_DTYPE)
 smp['offset'] = offs[idx]; smp['size'] = sizes[idx]; smp['height'] = hs[idx]; smp['width'] = ws[idx]
 d_smp = torch.from_numpy(smp.view(np.uint8)).to(dev)

@@ -2607,6 +2607,9 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
       return;
     }
   }
+  // diagnostics (K1's stamp buffer, slot 11): bands of this image that take
+  // the general path below
+  if (a.dbg && t == 0) atomicAdd((unsigned long long *)(a.dbg + (uint64_t)k * 16 + 11), 1ull);
   // LDS: [LUT][column + row taps][component tiles][RGB rows].  The taps of
   // the band's rows and of every output column are computed once per
   // workgroup; the tiles cover every plane sample the band's upsampling

@@ -65,3 +65,7 @@ wg_end = e.max(1, keepdims=True); wg_start = s0.min(1, keepdims=True)
 busy = (e - s0).sum(); held = (wg_end - s0).sum()
 print(f'workgroup hold: busy wave-time {busy / 100:.0f} us, held {held / 100:.0f} us, idle fraction {1 - busy / held:.3f}')
 print(f'per-image busy us: mean {((e - s0) / 100).mean():.1f} cv {((e - s0).std() / (e - s0).mean()):.3f}')
+# K2 bands on the general path (slot 11, counted by jpeg_color_resize_kernel)
+nb = (224 + 15) // 16
+g = d[:, 11]
+print(f'K2 general-path bands: {g.sum()} of {B * nb} ({g.sum() / (B * nb):.3f}); images with any: {(g > 0).mean():.3f}')

@@ -914,6 +914,7 @@ struct JpegArgs {
   const ffcv_sample *table;
   uint64_t n_table;
   const uint64_t *ids;
+  const uint32_t *k1_order;  // K1's image of (workgroup, wave) slot i (null: i itself); see k1_order_kernel
   ffcv_sample *samples_out;
   ffcv_draw_params dp;
   int do_draw;
@@ -1541,6 +1542,42 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
   return FFCV_SAMPLE_OK;
 }
 
+// K1 workgroup order: a workgroup's waves decode JW images and its LDS is
+// held until the slowest one is done, so images of similar stream length
+// (the best predictor of an image's K1 time) are grouped together: a
+// one-workgroup counting sort of the batch by compressed size in 1 KB
+// buckets.  Only which wave decodes which image changes: every image is
+// decoded the same way, and its outputs stay at its own index.
+#define K1O_NB 128
+__global__ void __launch_bounds__(1024) k1_order_kernel(JpegArgs a, uint32_t *order) {
+  __shared__ uint32_t cnt[K1O_NB];
+  const int t = threadIdx.x;
+  if (t < K1O_NB) cnt[t] = 0;
+  __syncthreads();
+  auto bucket = [&](int k) -> int {
+    uint64_t size = 0;
+    if (a.table) {
+      const uint64_t id = a.ids[k];
+      size = id < a.n_table ? a.table[id].size : 0;
+    } else {
+      size = a.samples[k].size;
+    }
+    return (int)min<uint64_t>(size >> 10, K1O_NB - 1);
+  };
+  for (int k = t; k < a.batch; k += blockDim.x) atomicAdd(&cnt[bucket(k)], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int b = 0; b < K1O_NB; b++) {
+      const uint32_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int k = t; k < a.batch; k += blockDim.x) order[atomicAdd(&cnt[bucket(k)], 1u)] = (uint32_t)k;
+}
+
 template <int MODE>
 // Waves per SIMD K1 is compiled for: 4 (= the LDS limit, 16 images per CU)
 // caps it at 128 VGPRs (a few spill, outside the decode loops); measured
@@ -1553,7 +1590,8 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const int wi = threadIdx.x / JL;  // image within the workgroup
   const int t = threadIdx.x % JL;   // lane within the image's segment
   const int sg = (threadIdx.x % JT) / JL;  // segment within the wave
-  const int k = blockIdx.x * (JW * IPW) + wi;
+  const int slot = blockIdx.x * (JW * IPW) + wi;
+  const int k = a.k1_order && slot < a.batch ? (int)wuni(a.k1_order[slot]) : slot;
   JShared &S = KS.w[wi];
   const bool have = k < a.batch;
   ffcv_sample smp = {};
@@ -2837,6 +2875,8 @@ struct ffcv_jpeg_ctx {
   ImgInfo *info;
   uint2 *taps;
   uint8_t *gtab;
+  uint32_t *k1_order;  // max_batch slots (k1_order_kernel); used when k1_sorted
+  bool k1_sorted;
   uint64_t gtab_slot;
   uint32_t *eidx;  // entropy index (caller-owned), or NULL
   uint64_t eidx_n;
@@ -2862,6 +2902,7 @@ static void free_ctx(ffcv_jpeg_ctx *c) {
   (void)hipFree(c->info);
   (void)hipFree(c->taps);
   (void)hipFree(c->gtab);
+  (void)hipFree(c->k1_order);
   delete c;
 }
 
@@ -2885,6 +2926,10 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   ffcv_jpeg_ctx *c = new ffcv_jpeg_ctx();
   c->max_batch = max_batch;
   c->diag_only = 7;
+  {
+    const char *o = getenv("FFCV_K1_ORDER");  // size-grouped K1 workgroups (A/B knob: 0 turns it off)
+    c->k1_sorted = !o || atoi(o) != 0;
+  }
   c->max_h = max_height;
   c->max_w = max_width;
   c->max_bytes = max_bytes;
@@ -2899,6 +2944,7 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
       (e = hipMalloc(&c->info, sizeof(ImgInfo) * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->taps, sizeof(uint2) * K2_TAPS * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess ||
+      (e = hipMalloc(&c->k1_order, sizeof(uint32_t) * max_batch)) != hipSuccess ||
       // the memset above runs on the null stream, which the caller's
       // non-blocking streams do not wait for: finish it here (a first launch
       // on another stream read a stale counter left in reused memory and
@@ -3093,8 +3139,14 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   hipEvent_t *ev = c->tev_n < c->tev_cap ? c->tev + 4 * c->tev_n++ : nullptr;
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[0], s));
   if (only & 1) {
+    if (c->k1_sorted && batch > JW * IPW) {
+      hipLaunchKernelGGL(k1_order_kernel, dim3(1), dim3(1024), 0, s, a, c->k1_order);
+      FFCV_LAUNCH_CHECK("k1_order_kernel");
+      a.k1_order = c->k1_order;
+    }
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), K1_PAD,
                        s, a);
+    a.k1_order = nullptr;
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[1], s));

@@ -1546,8 +1546,10 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
 // held until the slowest one is done, so images of similar stream length
 // (the best predictor of an image's K1 time) are grouped together: a
 // one-workgroup counting sort of the batch by compressed size in 1 KB
-// buckets.  Only which wave decodes which image changes: every image is
-// decoded the same way, and its outputs stay at its own index.
+// buckets, largest first, so the launch's last workgroups (its tail, which
+// K1b and K2 wait for) hold its smallest images.  Only which wave decodes
+// which image changes: every image is decoded the same way, and its outputs
+// stay at its own index.
 #define K1O_NB 128
 __global__ void __launch_bounds__(1024) k1_order_kernel(JpegArgs a, uint32_t *order) {
   __shared__ uint32_t cnt[K1O_NB];
@@ -1562,7 +1564,11 @@ __global__ void __launch_bounds__(1024) k1_order_kernel(JpegArgs a, uint32_t *or
     } else {
       size = a.samples[k].size;
     }
+#ifdef K1O_ASCENDING
     return (int)min<uint64_t>(size >> 10, K1O_NB - 1);
+#else
+    return K1O_NB - 1 - (int)min<uint64_t>(size >> 10, K1O_NB - 1);
+#endif
   };
   for (int k = t; k < a.batch; k += blockDim.x) atomicAdd(&cnt[bucket(k)], 1u);
   __syncthreads();

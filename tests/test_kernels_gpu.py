@@ -526,6 +526,56 @@ def test_jpeg_rrc_fused_matches_staged(hip_lib, oracle):
         assert np.array_equal(res[1][4][k], want[0]), k
 
 
+def test_jpeg_k1_order_is_output_neutral(hip_lib, oracle, monkeypatch):
+    """K1's size-grouped workgroup order (k1_order_kernel, FFCV_K1_ORDER, on
+    by default) only changes which wave decodes which image: crops, cutout,
+    flips, status and pixels equal those of the plain order, bit for bit,
+    across a batch of mixed sizes with an out-of-range id."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(57)
+    imgs, blobs = _jpeg_set(rng, 40)
+    buf, offs, sizes = pack(blobs)
+    hs = [i.shape[0] for i in imgs]
+    ws = [i.shape[1] for i in imgs]
+    table = _samples(offs, sizes, hs, ws, np.zeros(len(imgs)))
+    d_buf, d_table = _upload(buf), _dev(table)
+    ids = rng.integers(0, len(imgs), 75).astype(np.int64)
+    ids[11] = 10 ** 6  # out of range
+    B = len(ids)
+    d_ids = torch.from_numpy(ids).to('cuda:0')
+    dp = L.DrawParams()
+    dp.out_h = dp.out_w = 224
+    dp.cutout_size = 32
+    dp.scale[0], dp.scale[1] = 0.08, 1.0
+    dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
+    dp.loader_seed = 3
+    dp.epoch = 1
+    dp.flip_prob = 0.5
+    lut = torch.from_numpy(np.arange(256 * 3, dtype=np.int16) * 7).to('cuda:0')
+    rp = L.RRCParams()
+    rp.out_h = rp.out_w = 224
+    rp.cutout_size = 32
+    rp.lut = lut.data_ptr()
+    res = []
+    for order in ('0', '1'):
+        monkeypatch.setenv('FFCV_K1_ORDER', order)
+        dec = L.JpegDecoder(B, max(hs), max(ws), max(len(b) for b in blobs))
+        crops = torch.zeros((B, 4), dtype=torch.int32, device='cuda:0')
+        cut = torch.zeros((B, 2), dtype=torch.int32, device='cuda:0')
+        flips = torch.zeros((B,), dtype=torch.uint8, device='cuda:0')
+        out = torch.zeros((B, 224, 224, 3), dtype=torch.float16, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        dec.rrc_fused(d_buf, d_table, d_ids, dp, crops, cut, flips, rp, out, status)
+        torch.cuda.synchronize()
+        res.append([x.cpu().numpy() for x in (crops, cut, flips, out.view(torch.int16), status)])
+        del dec
+    for n, a_, b_ in zip(['crops', 'cut', 'flips', 'out', 'status'], *res):
+        assert np.array_equal(a_, b_), n
+    st = res[1][4]
+    assert st[11] != 0 and (np.delete(st, 11) == 0).all()
+
+
 def test_jpeg_entropy_index(hip_lib, oracle):
     """ffcv_jpeg_set_entropy_index: a fused launch with the index attached
     publishes one record per good sample (a duplicate id in the launch

@@ -62,7 +62,9 @@
 #endif
 #define IPW (JT / JL)   // images per wave
 #define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
+#ifndef FB_AC
 #define FB_AC 11        // first-level bits, the scan's first AC table (luma)
+#endif
 #define FB_AC2 10       // first-level bits, further AC tables (chroma)
 #ifndef FB_DC
 #define FB_DC 8         // first-level bits, DC tables

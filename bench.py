@@ -336,7 +336,11 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     gpu = local % ndev
     backend = os.environ.get('FFCV_BENCH_BACKEND', 'nccl')
-    if world > 1:
+    # a process group whenever the job is launched by torchrun (RANK and
+    # MASTER_ADDR in the environment), world size 1 included: the N > 1 path
+    # (RCCL init, barrier, max-over-ranks timing, per-rank gather) is then
+    # exercised on a 1-GPU box (tests/test_loader_gpu.py::test_bench_rccl_world1)
+    if world > 1 or ('RANK' in os.environ and 'MASTER_ADDR' in os.environ):
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         if backend == 'nccl':

@@ -20,7 +20,10 @@
 // and the tjTransform crop / flip (enable_crop, hflip) are not supported
 // either: ffcv passes the image's own size and False, False, 1, 1.
 #include <atomic>
+#include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -62,13 +65,18 @@ void build_huff(Huff &h, bool dc) {
   std::memset(h.look, 0, sizeof(h.look));
   for (int l = 1; l <= 16; l++) {
     h.valoff[l] = k - code;
+    // jpeg_make_d_derived_tbl rejects an over-subscribed length before any
+    // lookup entry is built: a code past 2^l - 1 would index past look[]
+    if (code + (int)h.bits[l] >= (1 << l)) {
+      h.bad = true;
+      break;
+    }
     for (int i = 0; i < h.bits[l]; i++, k++, code++)
       if (l <= kLook) {
         const int lo = code << (kLook - l), n = 1 << (kLook - l);
         for (int j = 0; j < n; j++) h.look[lo + j] = (uint16_t)(l << 8 | h.vals[k]);
       }
     h.maxcode[l] = h.bits[l] ? code - 1 : -1;
-    if (code >= (1 << l)) h.bad = true;
     code <<= 1;
   }
   h.maxcode[17] = 0x7fffffff;
@@ -157,6 +165,10 @@ const char *parse(const uint8_t *b, size_t n, Dec &d) {
         d.hmax = std::max(d.hmax, c.h);
         d.vmax = std::max(d.vmax, c.v);
       }
+      // non-integral ratios (e.g. luma h=3, chroma h=2): libjpeg's
+      // JERR_FRACT_SAMPLE_NOTIMPL, and the device parser's rejection
+      for (int i = 0; i < d.nc; i++)
+        if (d.hmax % d.c[i].h || d.vmax % d.c[i].v) return "unsupported sampling factors";
       sof = true;
     } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
       return "progressive / lossless / arithmetic coding is not supported";
@@ -608,6 +620,19 @@ int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes, con
     return FFCV_EINVAL;
   }
   std::atomic<int> next{0};
+  // the first failing sample's message: set_error is thread-local, so a
+  // worker's message is copied here and re-raised on the calling thread
+  std::mutex err_mu;
+  int err_k = batch;
+  std::string err_msg;
+  auto fail = [&](int k, const char *msg) {
+    status[k] = -1;
+    std::lock_guard<std::mutex> g(err_mu);
+    if (k < err_k) {
+      err_k = k;
+      err_msg = msg;
+    }
+  };
   auto work = [&]() {
     std::vector<uint8_t> img;
     for (int k = next.fetch_add(1); k < batch; k = next.fetch_add(1)) {
@@ -623,10 +648,16 @@ int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes, con
           o = img.data();
         }
         if (imdecode(const_cast<uint8_t *>(data[k]), sizes[k], h, w, o, h, w, 0, 0, 1, 1, false, false) != 0) {
-          status[k] = -1;
+          fail(k, ffcv_last_error());
           continue;
         }
         src = o;
+      } else if (sizes[k] < (uint64_t)h * w * 3) {  // a truncated / mislabelled raw sample
+        char buf[160];
+        snprintf(buf, sizeof(buf), "raw sample %d holds %llu bytes, %ux%ux3 needs %llu", k,
+                 (unsigned long long)sizes[k], h, w, (unsigned long long)h * w * 3);
+        fail(k, buf);
+        continue;
       } else if (!crops) {
         std::memcpy(dst, src, (size_t)h * w * 3);
         continue;
@@ -644,6 +675,7 @@ int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes, con
   for (int t = 1; t < T; t++) th.emplace_back(work);
   work();
   for (auto &x : th) x.join();
+  if (err_k < batch) ffcv::set_error("sample %d: %s", err_k, err_msg.c_str());
   return FFCV_OK;
 }
 

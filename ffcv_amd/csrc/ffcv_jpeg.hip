@@ -140,6 +140,9 @@ struct ImgInfo {
   uint32_t lane_blk0[64];
   int32_t lane_off[3][64];
   int16_t qmul[3][64] __attribute__((aligned(16)));
+  // this image's launch-arena reservation [arena_base, arena_base +
+  // arena_need) (need 0: none); read only by ffcv_jpeg_arena_regions
+  uint64_t arena_base, arena_need;
 };
 
 // Linear taps (resize.cpp linear coefficients, LinTap) packed in 8 bytes:
@@ -1509,7 +1512,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 // block, coefficient output only), window planes (64 B per block), K2 band
 // staging (crop RGB).
 FFCV_DEV uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
-FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t, int MODE) {
+FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t, int MODE, int k) {
   const uint64_t ds = align256((uint64_t)nbytes + 64), cf = align256((uint64_t)S.nwin * 128);
   // DC differences are stored only for the coefficient output (the other
   // modes predict DC from the write pass's per-lane running sums)
@@ -1522,10 +1525,23 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
   // 2^31 would otherwise sign-extend and read as TOO_LARGE)
   base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
-  if (base + need > a.arena_bytes) {  // arena exhausted: give the space back, so one huge image
-    // does not fail every image that allocates after it
-    if (t == 0) atomicAdd(a.arena_top, (unsigned long long)0 - (unsigned long long)need);
+  if (base + need > a.arena_bytes) {
+    // Arena exhausted.  Give the space back only if no reservation was made
+    // after this one (the counter still ends at this image's region): a
+    // compare-and-swap from base + need to base.  A plain subtract (round 3)
+    // lowered the counter below a later image's live region whenever two
+    // failures interleaved with a success, and the next image was handed
+    // overlapping scratch.  When the swap fails the region stays reserved
+    // (unused): the counter never goes below a live region.
+    if (t == 0) {
+      atomicCAS(a.arena_top, (unsigned long long)(base + need), (unsigned long long)base);
+      a.info[k].arena_need = 0;
+    }
     return FFCV_SAMPLE_TOO_LARGE;
+  }
+  if (t == 0) {
+    a.info[k].arena_base = base;
+    a.info[k].arena_need = need;
   }
   S.ds_off = base;
   S.ds_bytes = (uint32_t)ds;
@@ -1666,7 +1682,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   if (t == 0) S.src = src;
   if (JL == JT || t == 0) {  // the whole wave runs the (scalar) parse; see parse_header
     int st = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, wave_uniform(src), nbytes, smp, a, k, MODE)) : -1;
-    if (st == FFCV_SAMPLE_OK) st = alloc_scratch(S, a, nbytes, t, MODE);
+    if (st == FFCV_SAMPLE_OK) st = alloc_scratch(S, a, nbytes, t, MODE, k);
     if (t == 0) S.status = st;
   }
   __syncthreads();
@@ -2302,7 +2318,12 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
     for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? a.p.lut[u * K2T + t] : (uint16_t)0;
   }
   const int band_rows_n = MODE == JM_RRC ? min(a.p.out_h - band * BAND, BAND) : 0;
-  const uint2 *ktaps = MODE == JM_RRC && a.taps ? a.taps + (uint64_t)k * K2_TAPS : nullptr;
+  // K1 writes an image's tap table only when out_w + out_h fits K2_TAPS: a
+  // larger output never reads it (and past the last image the index would
+  // leave the allocation)
+  const uint2 *ktaps = MODE == JM_RRC && a.taps && a.p.out_w + a.p.out_h <= K2_TAPS
+                           ? a.taps + (uint64_t)k * K2_TAPS
+                           : nullptr;
   uint2 rt_pre = make_uint2(0, 0);
   uint4 ct_pre = make_uint4(0, 0, 0, 0);
   if (ktaps) {
@@ -3052,6 +3073,32 @@ int ffcv_jpeg_lane_table(ffcv_jpeg_ctx *c, void *stream, int n, uint32_t *blk0, 
       for (int q = 0; q < 3; q++) off[192 * k + 64 * q + l] = h[k].lane_off[q][l];
     }
   }
+  delete[] h;
+  return FFCV_OK;
+}
+
+// Diagnostic hook (not in the public header): the arena reservation the last
+// launch's entropy kernel made for images [0, n) -- base offset and size in
+// bytes (size 0: the image reserved nothing) -- and the image record's status.
+int ffcv_jpeg_arena_regions(ffcv_jpeg_ctx *c, void *stream, int n, uint64_t *base, uint64_t *size,
+                            uint64_t *capacity) {
+  if (!c || n < 0 || n > c->max_batch || !base || !size) {
+    ffcv::set_error("ffcv_jpeg_arena_regions: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  hipStream_t s = ffcv::as_stream(stream);
+  ImgInfo *h = new ImgInfo[n > 0 ? n : 1];
+  hipError_t e = hipMemcpyAsync(h, c->info, sizeof(ImgInfo) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete[] h;
+    return ffcv::check_hip(e, "ffcv_jpeg_arena_regions");
+  }
+  for (int k = 0; k < n; k++) {
+    base[k] = h[k].arena_base;
+    size[k] = h[k].arena_need;
+  }
+  if (capacity) *capacity = c->arena_bytes;
   delete[] h;
   return FFCV_OK;
 }

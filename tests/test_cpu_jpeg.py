@@ -85,6 +85,25 @@ def test_cpu_imdecode_rejects(hip_lib):
     assert b'progressive' in L.lib().ffcv_last_error()
     # truncated stream: decodes (zeros past the end, like libjpeg's warning path), never crashes
     assert L.imdecode(blob[: len(blob) // 2], out, 40, 56) in (0, -1)
+    # an over-subscribed DHT with an unchanged symbol count
+    # (three 1-bit codes) is rejected before any lookup entry is built
+    b = bytes(blob)
+    dht = b.index(b'\xff\xc4') + 4  # Tc/Th byte of the first table
+    bits = dht + 1
+    assert b[bits] == 0 and b[bits + 2] >= 3, 'expected the standard luma DC table'
+    over = bytearray(b)
+    over[bits] = 3
+    over[bits + 2] -= 3
+    assert L.imdecode(np.frombuffer(bytes(over), np.uint8), out, 40, 56) == -1
+    assert b'Huffman' in L.lib().ffcv_last_error()
+    # non-integral sampling ratios (luma h = 3, chroma h = 2)
+    sof = b.index(b'\xff\xc0') + 2 + 2 + 6  # first component's id
+    assert b[sof + 1] == 0x22 and b[sof + 4] == 0x11
+    frac = bytearray(b)
+    frac[sof + 1] = 0x32
+    frac[sof + 4] = 0x21
+    assert L.imdecode(np.frombuffer(bytes(frac), np.uint8), out, 40, 56) == -1
+    assert b'sampling' in L.lib().ffcv_last_error()
 
 
 def test_cpu_decode_batch(hip_lib, oracle):
@@ -126,3 +145,11 @@ def test_cpu_decode_batch(hip_lib, oracle):
         got = full[k].reshape(-1)[:h * w * 3].reshape(h, w, 3)
         assert np.array_equal(got, decoded[k]), k
     assert not full[3].any()
+    # the first failing sample's message reaches the calling thread
+    assert b'sample 4' in L.lib().ffcv_last_error()
+    # a raw sample shorter than h x w x 3 fails, with no read past it
+    short = [s.copy() for s in srcs]
+    short[5] = short[5][:-7]
+    st = L.cpu_decode_batch(short, hs, ws, modes, full, nthreads=3)
+    assert st[5] == -1 and (np.delete(st, 5) == 0).all()
+    assert b'raw sample 5' in L.lib().ffcv_last_error()

@@ -368,7 +368,12 @@ def test_jpeg_coefficients_match_oracle(hip_lib, oracle):
         assert np.array_equal(o[k, :len(want)], want), f'sample {k}'
 
 
-def test_jpeg_rrc_matches_oracle(hip_lib, oracle):
+@pytest.mark.parametrize('out_hw', [(224, 224), (288, 300)])
+def test_jpeg_rrc_matches_oracle(hip_lib, oracle, out_hw):
+    """Fused JPEG RRC + Cutout + flip (+ fp16 LUT) against the oracle; 288 x
+    300 has out_w + out_h past K2_TAPS, where K1 writes no tap table and K2
+    must not read one (the prefetch read past the allocation)."""
+    OH, OW = out_hw
     torch = _torch()
     from ffcv_amd import libffcv as L
     rng = np.random.default_rng(23)
@@ -378,23 +383,23 @@ def test_jpeg_rrc_matches_oracle(hip_lib, oracle):
     hs = [i.shape[0] for i in imgs]
     ws = [i.shape[1] for i in imgs]
     crops, cut, flips = _draw(hip_lib, np.arange(B, dtype=np.uint64) + 1000, hs, ws, 9, 2, cutout=32,
-                              flip_p=0.5)
+                              flip_p=0.5, out=out_hw)
     dec = L.JpegDecoder(B, max(hs), max(ws), max(len(b) for b in blobs))
     lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
-    u8 = oracle.rrc_batch([(b, h, w, 0) for b, h, w in zip(blobs, hs, ws)], crops, 224, 224)
+    u8 = oracle.rrc_batch([(b, h, w, 0) for b, h, w in zip(blobs, hs, ws)], crops, OH, OW)
     d_crops = torch.from_numpy(crops).to('cuda:0')
     d_cut = torch.from_numpy(cut).to('cuda:0')
     d_flips = torch.from_numpy(flips).to('cuda:0')
     d_lut = torch.from_numpy(lut.view(np.int16)).to('cuda:0')
     for use_lut in (False, True):
         p = L.RRCParams()
-        p.out_h, p.out_w = 224, 224
+        p.out_h, p.out_w = OH, OW
         p.cutout_size = 32
         for i, f in enumerate((124, 116, 103)):
             p.cutout_fill[i] = f
         if use_lut:
             p.lut = d_lut.data_ptr()
-        out = torch.zeros((B, 224, 224, 3), dtype=torch.float16 if use_lut else torch.uint8, device='cuda:0')
+        out = torch.zeros((B, OH, OW, 3), dtype=torch.float16 if use_lut else torch.uint8, device='cuda:0')
         status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
         dec.rrc(d_buf, d_smp, B, d_crops, d_cut, d_flips, p, out, status)
         torch.cuda.synchronize()
@@ -724,6 +729,76 @@ def test_jpeg_arena_sizing_and_exhaustion(hip_lib, oracle):
                 assert np.array_equal(got, oracle.jpeg_decode(blobs[k])), k
             else:
                 assert not got.any()
+        dec.close()
+
+
+def _arena_regions(dec, n):
+    import ctypes
+    from ffcv_amd import libffcv as L
+    f = L.lib().ffcv_jpeg_arena_regions
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    base = np.zeros(n, np.uint64)
+    size = np.zeros(n, np.uint64)
+    cap = ctypes.c_uint64(0)
+    assert f(dec.handle, None, n, base.ctypes.data, size.ctypes.data, ctypes.byref(cap)) == 0
+    return base, size, int(cap.value)
+
+
+@pytest.mark.parametrize('k1_order', ['1', '0'])
+def test_jpeg_exhausted_arena_regions_disjoint(hip_lib, oracle, monkeypatch, k1_order):
+    """an exhausted arena must never hand two images
+    overlapping scratch.  Round 3's rollback (atomicAdd(-need)) lowered the
+    bump counter below a later image's live region when two failures
+    interleaved with a success, and a status-0 image decoded wrong pixels.
+    Whatever the timing, the reservations of the images that report status 0
+    must be pairwise disjoint and inside the arena; checked on launches that
+    mix large and small images (both K1 orders), over several arena sizes,
+    with every status-0 image bit-exact against libjpeg-turbo."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    monkeypatch.setenv('FFCV_K1_ORDER', k1_order)  # read when the context is made
+    rng = np.random.default_rng(43)
+    sizes = [(int(rng.integers(40, 100)), int(rng.integers(40, 100))) for _ in range(56)]
+    for i in range(0, 56, 7):  # every seventh image large: failures interleave with successes
+        sizes[i] = (int(rng.integers(500, 700)), int(rng.integers(500, 700)))
+    imgs = [natural_image(rng, h, w) for h, w in sizes]
+    blobs = [encode_jpeg(im, 90, '4:2:0') for im in imgs]
+    hs = np.array([i.shape[0] for i in imgs])
+    ws = np.array([i.shape[1] for i in imgs])
+    ns = np.array([len(b) for b in blobs])
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    B = len(imgs)
+    full = L.arena_for(hs, ws, ns, B)
+    mh, mw = int(hs.max()), int(ws.max())
+    stride = mh * mw * 3
+    want = [oracle.jpeg_decode(b) for b in blobs]
+    for frac in (0.15, 0.3, 0.5, 0.8):
+        dec = L.JpegDecoder(B, mh, mw, int(ns.max()), int(full * frac))
+        out = torch.zeros(B * stride, dtype=torch.uint8, device='cuda:0')
+        for rep in range(3):
+            status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+            out.zero_()
+            dec.decode(d_buf, d_smp, B, out, stride, status)
+            torch.cuda.synchronize()
+            st = status.cpu().numpy()
+            assert set(st.tolist()) <= {0, 3}, st
+            assert (st == 0).any(), (frac, st)
+            if frac <= 0.15:  # well short of the launch's need: some images must fail
+                assert (st == 3).any(), (frac, st)
+            base, size, cap = _arena_regions(dec, B)
+            ok = np.flatnonzero(st == 0)
+            assert (size[ok] > 0).all()
+            lo, hi = base[ok], base[ok] + size[ok]
+            assert (hi <= cap).all(), (frac, rep)
+            order = np.argsort(lo)
+            assert (lo[order][1:] >= hi[order][:-1]).all(), (frac, rep, lo[order], hi[order])
+            o = out.cpu().numpy()
+            for k in range(B):
+                got = o[k * stride:k * stride + hs[k] * ws[k] * 3].reshape(hs[k], ws[k], 3)
+                if st[k] == 0:
+                    assert np.array_equal(got, want[k]), (frac, rep, k)
+                else:
+                    assert not got.any(), (frac, rep, k)
         dec.close()
 
 

@@ -480,3 +480,29 @@ def test_kept_batches_survive_set_boundaries(tmpdir_m):
             ch.cuda.synchronize()
             for k, (a, ac, b, bc) in enumerate(kept):
                 assert ch.equal(a, ac) and ch.equal(b, bc), f'batch {k - len(kept) + 1} overwritten'
+
+
+def test_bench_rccl_world1():
+    """the N > 1 bench path's RCCL branch
+    (init_process_group('nccl', device_id=...), barrier, max-over-ranks
+    all-reduce of the timed region, per-rank all-gather) run once here, as a
+    torchrun job of world size 1, so it is not first executed on the 8-GPU
+    scaling node.  The line must carry process_group.backend == 'nccl' and a
+    green parity check."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = 29800 + os.getpid() % 100
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.join(root, 'bench.py'),
+           '--gpus', '1', '--steps', '6', '--warmup', '2', '--unique', '512', '--dataset-size', '40000',
+           '--no-cpu-baseline', '--no-later-epochs', '--no-c5', '--parity-rows', '256']
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
+    pg = line['process_group']
+    assert pg['backend'] == 'nccl' and pg['world_size'] == 1, pg
+    assert line['n_gpus'] == 1 and line['value'] > 0
+    assert line['parity']['checked'] > 0 and line['parity']['mismatch'] == 0

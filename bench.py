@@ -48,9 +48,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-# instruction (MI355X_MICROARCH.md "issues each VALU instruction over 2 cycles")
-VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU
+# instruction.  Measured on gfx950 (tools/op_rate, profiles/r3b_op_rate.txt):
+# the integer forms these kernels are made of -- 24-/32-bit multiplies,
+# v_bfe, v_perm, v_dot2, v_max/med3, v_add3, v_lshl_or, v_cndmask_e64,
+# 64-bit shifts -- issue one wave64 instruction per ~4 cycles per SIMD; only
+# the plain VOP2 add / and / shift and v_mul_f32 take ~2.  One peak for
+# every issue fraction in the line: 614.4 G wave-instructions/s.
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 4
 
 CONFIGS = {
     # name: (mode, max_side, out, batch, cutout, normalize, dataset_size)
@@ -245,7 +250,7 @@ def parity_check(cfg, slots, order, batch, tile, offs, sizes, hs, ws, rows_total
                     'required, checked after the timed region'}
 
 
-def sub_result(config, timeout_s=150):
+def sub_result(config, timeout_s=240):
     """The other device-resident BASELINE configs measured beside the
     headline, never as `value` (BASELINE.md "device-resident img/s for C2, C3
     and C5"): this script in a child process with --config c5 (C5, "the
@@ -257,7 +262,7 @@ def sub_result(config, timeout_s=150):
     import subprocess
     unique = {'c5': '1024', 'c2': '10000'}[config]
     cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', config, '--steps', '200', '--warmup', '20',
-           '--unique', unique, '--no-cpu-baseline', '--no-later-epochs', '--parity-rows', '512']
+           '--unique', unique, '--cpu-budget', '5', '--no-later-epochs', '--parity-rows', '512']
     env = dict(os.environ)
     for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
         env.pop(k, None)
@@ -269,8 +274,8 @@ def sub_result(config, timeout_s=150):
     if r.returncode != 0 or not lines:
         return {'error': f'{config} run failed (rc {r.returncode}): {r.stderr.strip()[-400:]}'}
     d = json.loads(lines[-1])
-    keep = ('metric', 'value', 'unit', 'steps', 'warmup', 'ms_per_step', 'dtype', 'data', 'config', 'roofline',
-            'parity')
+    keep = ('metric', 'value', 'unit', 'steps', 'warmup', 'ms_per_step', 'dtype', 'arith_dtype', 'data', 'config',
+            'roofline', 'parity', 'cpu_baseline')
     out = {k: d[k] for k in keep if k in d}
     out['command'] = ' '.join(['bench.py'] + cmd[2:])
     return out
@@ -687,8 +692,12 @@ def main():
     hbm = {'bound': 'hbm', 'achieved': round(hbm_achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(hbm_achieved / HBM_PEAK_GBS, 5), 'traffic': None,
            'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note}
-    kernels = (['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', 'jpeg_color_resize_kernel<0, true>' if norm else
-                'jpeg_color_resize_kernel<0, false>'] if mode == 'jpg' else ['rrc_raw_kernel<false>'])
+    # K2: the per-band kernel, or the band-loop kernel with FFCV_K2_LOOP=1
+    # (the library reads the same variable)
+    k2_loop = os.environ.get('FFCV_K2_LOOP', '0').strip() not in ('0', '') and not args.k2flags
+    k2 = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>' if k2_loop else
+          f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
+    kernels = ['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', k2] if mode == 'jpg' else ['rrc_raw_kernel<false>']
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
     # (tools/profile.sh -> tools/pmc_summary.py): bytes per image x images per launch
     pm = load_profile(f'traffic_{args.config}.json')
@@ -722,8 +731,9 @@ def main():
                 'traffic': hbm['traffic'], **launch,
                 'valu_per_image': {n: round(sq[n]['valu_per_image'], 1) for n in kernels},
                 'note': (f'SQ_INSTS_VALU per image from profiles/sq_{args.config}.json (rocprofv3 --pmc, build '
-                         f'{sq.get("_build")}) x images/s; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 '
-                         f'VALU instruction'),
+                         f'{sq.get("_build")}) x images/s; peak = 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 '
+                         f'VALU instruction (the measured issue rate of the integer VOP3 forms, '
+                         f'profiles/r3b_op_rate.txt)'),
                 'hbm': hbm}
         if kernel_ms is not None and kernel_imgs:
             # Per kernel (VERDICT r2 "next" 3): durations from the HIP events
@@ -732,13 +742,11 @@ def main():
             # duration includes time it shares with the other streams' kernels,
             # as rocprofv3's kernel trace does), counters from the committed
             # rocprofv3 passes.  issue = SQ_INSTS_VALU per image / ns per image
-            # against 1.2288 wave-instructions per ns (2 cycles per wave64 VALU
-            # instruction; the VOP3 integer forms this code is made of take ~4,
-            # tools/op_rate, so the issue-bound fraction lies between frac and
-            # frac_vop3).  hbm_frac_alg = SURVEY 8(d)'s whole-path algorithmic
+            # against 0.6144 wave-instructions per ns (4 cycles per wave64 VALU
+            # instruction, VALU_PEAK_GIPS).  hbm_frac_alg = SURVEY 8(d)'s whole-path algorithmic
             # bytes per image over this kernel's time; hbm_frac_counter = its
             # own FETCH_SIZE + WRITE_SIZE per image over its time.
-            # (ns per image -> VALU wave-instr per ns = G/s against 1228.8 G/s;
+            # (ns per image -> VALU wave-instr per ns = G/s against 614.4 G/s;
             # bytes per ns = GB/s against 8000 GB/s)
             per = {}
             for i, n in enumerate(kernels):
@@ -750,7 +758,6 @@ def main():
                      'isolated_images_per_launch': cap,
                      'valu_per_image': round(q['valu_per_image'], 1),
                      'issue_frac': round(q['valu_per_image'] / ns_img / VALU_PEAK_GIPS, 4),
-                     'issue_frac_vop3': round(2 * q['valu_per_image'] / ns_img / VALU_PEAK_GIPS, 4),
                      'hbm_frac_alg': round(unit_bytes / ns_img / HBM_PEAK_GBS, 4),
                      'ns_per_image_overlapped': round(ns_ov, 2),
                      'launch_ms_overlapped': round(kernel_ms[i] / n_launch, 4),
@@ -790,8 +797,8 @@ def main():
                     'dominant_kernel': dom, **launch,
                     'limiter': (f'{dom}: {d.get("us_per_wave_at_2.4GHz", "?")} us per wave (one image per wave), '
                                 f'{100 * d.get("wait_frac", 0):.0f}% of wave cycles waiting; VALU issue '
-                                f'{d["issue_frac"]:.3f} of the 2-cycle peak ({d["issue_frac_vop3"]:.3f} at the '
-                                f'~4-cycle VOP3 cost); HBM {d["hbm_frac_alg"]:.3f} of 8 TB/s by algorithmic bytes, '
+                                f'{d["issue_frac"]:.3f} of the 4-cycle peak; HBM {d["hbm_frac_alg"]:.3f} of '
+                                f'8 TB/s by algorithmic bytes, '
                                 f'{d.get("hbm_frac_counter", 0):.3f} by its own counter bytes'),
                     'note': ('dominant kernel (largest isolated time per image): achieved = its SQ_INSTS_VALU per '
                              'image (profiles/sq_*.json) / its ns per image from HIP events recorded around it on its '
@@ -800,6 +807,12 @@ def main():
                              'overlapped launches and the rocprofv3 profile\'s avg_ns; traffic = its FETCH_SIZE + '
                              'WRITE_SIZE per image x images per launch (profiles/traffic_*.json)'),
                     'per_kernel': per, 'path': path, 'hbm': hbm}
+    if 'per_kernel' not in roof and kernel_ms is not None and kernel_imgs:
+        # no committed counters for these kernels (a new build): durations only
+        roof['per_kernel'] = {n: {'ns_per_image_isolated': round((iso_ms[i] * 1e6 / iso_imgs) if iso_ms is not None
+                                                                 else kernel_ms[i] * 1e6 / kernel_imgs, 2),
+                                  'ns_per_image_overlapped': round(kernel_ms[i] * 1e6 / kernel_imgs, 2)}
+                              for i, n in enumerate(kernels)}
     res = {
         'metric': 'device-resident images/s, JPEG->RRC 224x224 batch 512; HBM GB/s vs peak',
         'value': round(value, 1),
@@ -812,7 +825,11 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'u8',
+        # output element type; the arithmetic is integer (Huffman, ifast IDCT,
+        # fixed-point colour, Q11 INTER_AREA) with an fp16 LUT for Normalize
+        'dtype': 'fp16' if (mode == 'jpg' and norm) else 'u8',
+        'arith_dtype': ('int32 (Huffman, ifast IDCT, fixed-point colour, Q11 / f32 INTER_AREA)'
+                        + (' + fp16 LUT normalize' if norm else '')),
         'data': f'synthetic ({U} unique encodings replicated to {N} HBM-resident samples)',
         'config': {'workload': WORKLOAD[args.config], 'global_batch': batch * world,
                    'per_gpu_batch': batch, 'batches_per_launch': G, 'launches_in_flight': S,

@@ -89,24 +89,34 @@ struct LdsSrc {
 #ifndef RRC_WPE
 #define RRC_WPE 5  // waves per SIMD the raw kernel is compiled for (5 workgroups per CU by LDS)
 #endif
+// LDS of one band (the per-band kernel's, and the band-loop kernel's for the
+// bands it hands to rrc_band)
 template <bool FP16>
-__global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_eu(RRC_WPE)))
-    rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
-                   const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
-                   const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
-                   void *__restrict__ out) {
-  __shared__ uint16_t s_lut[FP16 ? 768 : 1];
-  __shared__ uint4 s_src[RRC_LDS_BYTES / 16];
-  __shared__ uint4 s_rt[RRC_BAND];  // linear row taps: {ra, rb, c0 << 8, c1 << 8}
-  __shared__ AreaTaps s_at[RRC_BAND];
-  const int k = blockIdx.y;
+struct RrcLds {
+  uint16_t lut[FP16 ? 768 : 1];
+  uint4 src[RRC_LDS_BYTES / 16];
+  uint4 rt[RRC_BAND];  // linear row taps: {ra, rb, c0 << 8, c1 << 8}
+  AreaTaps at[RRC_BAND];
+};
+
+// One band of RRC_BAND output rows of image k.  Every barrier is reached by
+// all threads; thread-level returns follow the last one.
+template <bool FP16>
+FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
+                       const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
+                       const uint8_t *__restrict__ flips, const ffcv_rrc_params &p, uint64_t stride,
+                       void *__restrict__ out, const int k, const int band, RrcLds<FP16> &S) {
+  uint16_t *s_lut = S.lut;
+  uint4 *s_src = S.src;
+  uint4 *s_rt = S.rt;
+  AreaTaps *s_at = S.at;
   const int t = threadIdx.x;
   const ffcv_sample s = samples[k];
   if (FP16) {
     for (int i = t; i < 768; i += RRC_THREADS) s_lut[i] = p.lut[i];
   }
   if (s.mode != 1) return;
-  const int oy0 = blockIdx.x * RRC_BAND, oy1 = min(p.out_h, oy0 + RRC_BAND);
+  const int oy0 = band * RRC_BAND, oy1 = min(p.out_h, oy0 + RRC_BAND);
   if (oy0 >= p.out_h) return;
   const int ci = crops[4 * k], cj = crops[4 * k + 1], chh = crops[4 * k + 2], cww = crops[4 * k + 3];
   GlobalSrc src{base + s.offset + ((uint64_t)ci * s.width + cj) * 3, (uint64_t)s.width * 3};
@@ -437,6 +447,16 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
     }
     store_px<FP16>(o, (uint64_t)dy * out_w + dx, v, s_lut);
   }
+}
+
+template <bool FP16>
+__global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_eu(RRC_WPE)))
+    rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
+                   const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
+                   const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
+                   void *__restrict__ out) {
+  __shared__ RrcLds<FP16> S;
+  rrc_band<FP16>(base, samples, crops, cut, flips, p, stride, out, (int)blockIdx.y, (int)blockIdx.x, S);
 }
 
 // --------------------------------------------- simple (raw) gather -------

@@ -624,6 +624,30 @@ def main():
         sl0['dec'].set_timing(0)
         sl0['last'] = None
 
+    # Raw path (C5): the kernel's own launch duration -- launches of G
+    # batches run one at a time after the timed region, HIP events on the
+    # launch's stream around rrc_raw_kernel only -- so the roofline's
+    # `achieved` is the kernel's rate (the timed region's launches overlap on S
+    # streams, which inflates each launch's event duration), and a rocprofv3
+    # run of the same launches with --inflight 1 reproduces it from avg_ns
+    raw_iso_ms, raw_iso_imgs = None, 0
+    if mode != 'jpg' and not args.no_kernel_events:
+        sl0 = slots[0]
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        raw_iso_ms = 0.0
+        for r in range(3):
+            b0 = (r * G) % prime_batches
+            ids = d_order[b0 * batch:(b0 + G) * batch]
+            L.gather_samples(d_table, ids, sl0['smp'], streams[0])
+            L.draw_batch(ids, sl0['smp'], dp, sl0['crops'], sl0['cut'], None, sl0['rstat'], streams[0])
+            ev0.record(streams[0])
+            L.rrc_raw_batch(d_data, sl0['smp'], cap, sl0['crops'], sl0['cut'], None, rp, sl0['out'], streams[0])
+            ev1.record(streams[0])
+            streams[0].synchronize()
+            raw_iso_ms += ev0.elapsed_time(ev1)
+            raw_iso_imgs += cap
+        sl0['last'] = None
+
     # Later epochs (reported beside the headline, never as `value`): the
     # Loader's default entropy index (768 B of HBM per sample) records where
     # each lane range of the Huffman decode starts the first time a sample is
@@ -719,6 +743,17 @@ def main():
               'launches': n_launch, 'launch_ms': round(eff_launch_ms, 4),
               'launch_ms_events': round(float(np.mean(launch_ms)), 4)}
     roof = dict(hbm, **launch)
+    if raw_iso_ms:
+        # achieved = algorithmic bytes per launch / the kernel's own launch
+        # duration (isolated launches, above); the whole job's rate beside it
+        ns_img = raw_iso_ms * 1e6 / raw_iso_imgs
+        roof.update(achieved=round(unit_bytes / ns_img, 2), frac=round(unit_bytes / ns_img / HBM_PEAK_GBS, 5),
+                    kernel_ns_per_image_isolated=round(ns_img, 2), isolated_images_per_launch=cap,
+                    kernel_launch_ms_isolated=round(ns_img * cap / 1e6, 4),
+                    achieved_job=hbm['achieved'], frac_job=hbm['frac'],
+                    note=roof_note + '; achieved = that x images per launch / rrc_raw_kernel\'s own duration '
+                                     '(HIP events, 3 launches of G batches one at a time after the timed region); '
+                                     'achieved_job = the same bytes x the timed region\'s images/s')
     sq = load_profile(f'sq_{args.config}.json')
     if mode == 'jpg' and sq and all(n in sq for n in kernels):
         # the JPEG path is bound by instruction issue / latency of the serial

@@ -716,9 +716,13 @@ def main():
     hbm = {'bound': 'hbm', 'achieved': round(hbm_achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(hbm_achieved / HBM_PEAK_GBS, 5), 'traffic': None,
            'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note}
-    # K2: the per-band kernel, or the band-loop kernel with FFCV_K2_LOOP=1
-    # (the library reads the same variable)
-    k2_loop = os.environ.get('FFCV_K2_LOOP', '0').strip() not in ('0', '') and not args.k2flags
+    # K2: the library runs the band-loop kernel for launches of >= 8,192
+    # images (FFCV_K2_LOOP=1: always, =0: never), the per-band one otherwise;
+    # the per-kernel roofline names the one its isolated launches (cap images,
+    # as the rocprofv3 passes' uniform launches) ran
+    k2e = os.environ.get('FFCV_K2_LOOP')
+    k2_min = 8192 if k2e is None else (0 if k2e.strip() not in ('0', '') else 1 << 62)
+    k2_loop = cap >= k2_min and not args.k2flags
     k2 = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>' if k2_loop else
           f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
     kernels = ['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', k2] if mode == 'jpg' else ['rrc_raw_kernel<false>']

@@ -50,6 +50,8 @@
 //
 // Every integer step matches libjpeg-turbo bit for bit
 // (tests/test_kernels_gpu.py); float steps use -ffp-contract=off.
+#include <climits>
+
 #include "api_internal.h"
 #include "device_common.h"
 
@@ -2196,6 +2198,7 @@ struct ColorGeom {
 static_assert(K2REC_DW <= 64, "record head fits one wave's lanes");
 struct K2Rec {
   uint32_t w;  // this lane's dword of the record head
+  FFCV_DEV void load(const ImgInfo *rec, int t) { w = (t & 63) < K2REC_DW ? ((const uint32_t *)rec)[t & 63] : 0u; }
   FFCV_DEV uint32_t u(int i) const { return (uint32_t)__builtin_amdgcn_readlane((int)w, i); }
   FFCV_DEV int32_t s(int i) const { return (int32_t)u(i); }
   FFCV_DEV uint64_t u64(int i) const { return (uint64_t)u(i) | ((uint64_t)u(i + 1) << 32); }
@@ -2311,7 +2314,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   // the record head, the LUT, this band's row taps, this thread's column
   // taps and the epilogue draws (see K2Rec)
   K2Rec R;
-  R.w = (t & 63) < K2REC_DW ? ((const uint32_t *)(a.info + k))[t & 63] : 0u;
+  R.load(a.info + k, t);
   constexpr int LU = (768 + K2T - 1) / K2T;
   uint16_t lv[LU];
   if (FP16) {
@@ -2953,13 +2956,13 @@ FFCV_DEV K2Band k2l_band_geom(const ImgInfo &I, const ResizePlan &P, int oy0, in
 // RGBx rows the walk reads and does not wait for the loads in flight before
 // each of those reads; the LUT and RGBx rows in the dynamic area.
 #ifndef K2L_TILE
-#define K2L_TILE 9216  // a band's plane tiles (4:2:0, crop width <= 256: <= 8.8 KB)
+#define K2L_TILE 8192  // a band's plane tiles (4:2:0: <= 8 KB; bigger bands take the general path)
 #endif
 #ifndef K2L_DYN
-#define K2L_DYN 22528  // [LUT 1.5 KB][RGBx rows <= 20.5 KB]; with the tiles 31 KB: 5 workgroups per CU
+#define K2L_DYN 18432  // [LUT 1.5 KB][RGBx rows <= 16.5 KB]; with the tiles 26 KB: 6 workgroups per CU
 #endif
 #ifndef K2L_WPE
-#define K2L_WPE 5
+#define K2L_WPE 6  // (5 workgroups per CU at 31 KB measured 1% slower)
 #endif
 #ifndef K2L_BPW
 #define K2L_BPW 7  // bands per workgroup (an image's 14 bands of 224 rows in two workgroups)
@@ -2986,7 +2989,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   const int nb = (out_h + BAND - 1) / BAND;
   const int b0 = blockIdx.x * K2L_BPW, b1 = min(nb, b0 + K2L_BPW);  // this workgroup's bands
   K2Rec R;
-  R.w = (t & 63) < K2REC_DW ? ((const uint32_t *)(a.info + k))[t & 63] : 0u;
+  R.load(a.info + k, t);
   constexpr int LU = (768 + K2T - 1) / K2T;
   uint16_t lv[LU];
   if (FP16) {
@@ -3282,7 +3285,7 @@ struct ffcv_jpeg_ctx {
   uint8_t *gtab;
   uint32_t *k1_order;  // max_batch slots (k1_order_kernel); used when k1_sorted
   bool k1_sorted;
-  bool k2_loop;  // RRC launches run K2 as jpeg_rrc_loop_kernel (one workgroup per image)
+  int k2_loop_min;  // RRC launches of at least this many images run K2 as jpeg_rrc_loop_kernel
   uint64_t gtab_slot;
   uint32_t *eidx;  // entropy index (caller-owned), or NULL
   uint64_t eidx_n;
@@ -3335,11 +3338,13 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   {
     const char *o = getenv("FFCV_K1_ORDER");  // size-grouped K1 workgroups (A/B knob: 0 turns it off)
     c->k1_sorted = !o || atoi(o) != 0;
-    // band-loop K2 (opt-in, FFCV_K2_LOOP=1): +1.7-3% at 400 steps but -6% at
-    // the driver's 20 (its long workgroups hold LDS that the other streams'
-    // entropy workgroups wait for)
+    // band-loop K2 for launches of at least k2_loop_min images (DESIGN.md s6,
+    // round 4: +2.8% at C3's 12,288-image launches, -9% at the driver's
+    // 2,048-4,096: with few images per launch its long workgroups hold LDS the
+    // other streams' entropy workgroups wait for, and end the launch in a
+    // coarser tail).  FFCV_K2_LOOP=0 never, =1 always, unset: the size rule
     const char *l = getenv("FFCV_K2_LOOP");
-    c->k2_loop = l && atoi(l) != 0;
+    c->k2_loop_min = !l ? 8192 : (atoi(l) != 0 ? 0 : INT_MAX);
   }
   c->max_h = max_height;
   c->max_w = max_width;
@@ -3594,7 +3599,7 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[2], s));
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (!(only & 4)) {
-  } else if (c->k2_loop && !a.k2flags) {
+  } else if (batch >= c->k2_loop_min && !a.k2flags) {
     if (fp16)
       hipLaunchKernelGGL((jpeg_rrc_loop_kernel<true>), dim3((g2.x + K2L_BPW - 1) / K2L_BPW, batch), dim3(K2T),
                          K2L_DYN, s, a);

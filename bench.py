@@ -106,12 +106,23 @@ def make_unique(mode, side, n_unique, seed, workers):
         z = np.load(path)
         return z['tile'], z['offs'], z['sizes'], z['hs'], z['ws']
     jobs = [(i, mode, side, seed) for i in range(n_unique)]
+    # progress on stderr every ~10 s (a silent minutes-long generation on a
+    # fresh box reads as a hang to the GPU runner)
+    res, t_last = [], time.perf_counter()
     if workers > 1:
         import multiprocessing as mp
         with mp.get_context('fork').Pool(workers) as pool:
-            res = pool.map(_gen_one, jobs, chunksize=32)
+            for r in pool.imap(_gen_one, jobs, chunksize=32):
+                res.append(r)
+                if time.perf_counter() - t_last > 10:
+                    t_last = time.perf_counter()
+                    print(f'bench: generating samples {len(res)}/{n_unique}', file=sys.stderr, flush=True)
     else:
-        res = [_gen_one(j) for j in jobs]
+        for j in jobs:
+            res.append(_gen_one(j))
+            if time.perf_counter() - t_last > 10:
+                t_last = time.perf_counter()
+                print(f'bench: generating samples {len(res)}/{n_unique}', file=sys.stderr, flush=True)
     from ffcv_amd.synthetic import pack
     tile, offs, sizes = pack([r[0] for r in res])
     hs = np.array([r[1] for r in res], np.uint32)

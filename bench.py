@@ -770,6 +770,15 @@ def main():
                                      '(HIP events, 3 launches of G batches one at a time after the timed region); '
                                      'achieved_job = the same bytes x the timed region\'s images/s')
     sq = load_profile(f'sq_{args.config}.json')
+    if mode != 'jpg' and raw_iso_ms and sq and kernels[0] in sq:
+        # the raw kernel's VALU issue beside its HBM fraction: its exact
+        # fixed-point linear walk keeps the SIMDs issuing
+        v_img = sq[kernels[0]]['valu_per_image']
+        g = v_img / (raw_iso_ms * 1e6 / raw_iso_imgs)
+        roof['issue'] = {'valu_per_image': round(v_img, 1), 'achieved': round(g, 2), 'peak': VALU_PEAK_GIPS,
+                         'unit': 'G VALU wave-instr/s', 'frac': round(g / VALU_PEAK_GIPS, 4),
+                         'note': f'SQ_INSTS_VALU per image (profiles/sq_{args.config}.json, build {sq.get("_build")}) '
+                                 f'over the isolated ns per image; the 4-cycle peak as for C3'}
     if mode == 'jpg' and sq and all(n in sq for n in kernels):
         # the JPEG path is bound by instruction issue / latency of the serial
         # Huffman chain, not HBM: VALU wave-instructions per

@@ -1,5 +1,6 @@
 // ffcv_common.hip -- error state, device/stream/memory helpers and the
 // reference-compatible my_memcpy (libffcv.cpp:44-46).
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -75,6 +76,15 @@ int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stre
 
 // libffcv.cpp:44-46: my_memcpy(source, dst, size) -- host plumbing only.
 void my_memcpy(void *source, void *dst, uint64_t size) { std::memcpy(dst, source, size); }
+
+// libffcv.cpp:48-51: my_fread(fp, offset, destination, size) on a FILE *
+// passed as an integer -- host plumbing only.
+void my_fread(int64_t fp, int64_t offset, void *destination, int64_t size) {
+  FILE *f = (FILE *)(intptr_t)fp;
+  if (!f || size <= 0) return;
+  if (fseeko(f, (off_t)offset, SEEK_SET) != 0) return;
+  (void)fread(destination, 1, (size_t)size, f);
+}
 
 // Host gather of n byte ranges (e.g. a batch's compressed samples out of the
 // mmap'd .beton) into one staging buffer, split over nthreads threads by

@@ -73,6 +73,7 @@ _SIGS = {
     'ffcv_memcpy_h2d_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     'ffcv_memcpy_d2h_async': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     'my_memcpy': (None, [c_void_p, c_void_p, c_uint64]),
+    'my_fread': (None, [ctypes.c_int64, ctypes.c_int64, c_void_p, ctypes.c_int64]),
     'resize': (None, [ctypes.c_int64] * 11),
     'imdecode': (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32,
                          c_uint32, c_uint32, c_uint32, c_uint32, ctypes.c_bool, ctypes.c_bool]),

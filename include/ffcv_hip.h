@@ -111,6 +111,12 @@ int ffcv_memcpy_d2h_async(void *dst, const void *src, uint64_t bytes, void *stre
  * CPU-only Loader, C1).  Same argument order as the reference. */
 void my_memcpy(void *source, void *dst, uint64_t size);
 
+/* libffcv.cpp:48-51 my_fread: fseek((FILE *)fp, offset, SEEK_SET) then
+ * fread(destination, 1, size, fp) (host plumbing; exported by the reference,
+ * never bound by its Python).  Same arguments; like the reference it returns
+ * nothing, and a short read leaves the rest of destination untouched. */
+void my_fread(int64_t fp, int64_t offset, void *destination, int64_t size);
+
 /* libffcv.cpp:33-42 resize: cv::resize(src[start_row:end_row,
  * start_col:end_col], dst, (tx rows, ty cols), INTER_AREA) where src is an
  * sx x sy x 3 uint8 image and dst a tx x ty x 3 uint8 buffer, both in host

@@ -112,6 +112,29 @@ def test_host_read_and_imdecode_arguments(tmp_path, hip_lib):
     assert L.imdecode(data, out, 8, 8, 0, 8) == -1
 
 
+def test_my_fread(tmp_path, hip_lib):
+    """libffcv.cpp:48-51 my_fread(FILE *, offset, destination, size): fseek + fread."""
+    p = tmp_path / 'f.bin'
+    data = np.random.default_rng(3).integers(0, 256, 5000, dtype=np.uint8)
+    p.write_bytes(data.tobytes())
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    fp = libc.fopen(str(p).encode(), b'rb')
+    assert fp
+    try:
+        for off, n in [(0, 100), (4321, 679), (17, 1), (1000, 3000)]:
+            dst = np.zeros(n, np.uint8)
+            hip_lib.my_fread(fp, off, dst.ctypes.data, n)
+            assert np.array_equal(dst, data[off:off + n])
+        dst = np.full(64, 7, np.uint8)  # short read at the end: the rest stays as it was
+        hip_lib.my_fread(fp, 4990, dst.ctypes.data, 64)
+        assert np.array_equal(dst[:10], data[4990:]) and (dst[10:] == 7).all()
+    finally:
+        libc.fclose(fp)
+
+
 def test_scratch_bound_matches_c(hip_lib):
     """libffcv.scratch_bound (numpy, used to size launch arenas) equals
     ffcv_jpeg_scratch_bound; arena_for sums the largest per-image bounds."""

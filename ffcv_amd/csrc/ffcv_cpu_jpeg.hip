@@ -16,9 +16,10 @@
 // components in one scan, any sampling factors 1..4, restart intervals.
 // Progressive, arithmetic, lossless, 12-bit, multi-scan and CMYK streams
 // return -1 (the device path reports FFCV_SAMPLE_UNSUPPORTED for them).
-// Requests whose size differs from the image's (TurboJPEG's scaled decode)
-// and the tjTransform crop / flip (enable_crop, hflip) are not supported
-// either: ffcv passes the image's own size and False, False, 1, 1.
+// The tjTransform crop / mirror (enable_crop, hflip) is restated on the
+// coefficients (transform_coefs); TurboJPEG's scaled decoding is not: a
+// request that TurboJPEG would decode at a factor other than 1/1 returns -1.
+// ffcv itself passes the image's own size and False, False, 1, 1.
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -419,11 +420,10 @@ struct Scratch {
 };
 thread_local Scratch t_scr;
 
-// Huffman decode + IDCT of the whole scan into the component planes.
-void decode_planes(const uint8_t *b, Dec &d, Scratch &S, int stride[3]) {
-  const Tables &T = tables();
+// Plane geometry of a decode: downsampled sizes, whole-MCU block grids, and
+// the ifast multipliers (jddctmgr.c) of each component.
+void plane_setup(Dec &d, Scratch &S, int stride[3], int16_t qm[3][64]) {
   const int mcux = (d.W + 8 * d.hmax - 1) / (8 * d.hmax), mcuy = (d.H + 8 * d.vmax - 1) / (8 * d.vmax);
-  int16_t qm[3][64];
   for (int i = 0; i < d.nc; i++) {
     Comp &c = d.c[i];
     c.cw = (d.W * c.h + d.hmax - 1) / d.hmax;
@@ -434,13 +434,21 @@ void decode_planes(const uint8_t *b, Dec &d, Scratch &S, int stride[3]) {
     S.plane[i].resize((size_t)stride[i] * c.bh * 8);
     for (int k = 0; k < 64; k++) qm[i][k] = (int16_t)(((int64_t)d.qt[c.tq][k] * kAanScales[k] + (1 << 11)) >> 12);
   }
+}
+
+// Huffman decode of the whole scan: emit(component, block x, block y,
+// coefficients in natural order with the absolute DC) for every coded block.
+template <class Emit>
+void decode_scan(const uint8_t *b, const Dec &d, Emit &&emit) {
+  const int mcux = (d.W + 8 * d.hmax - 1) / (8 * d.hmax), mcuy = (d.H + 8 * d.vmax - 1) / (8 * d.vmax);
   Bits br{b + d.ecs, b + d.ecs_end};
   int pred[3] = {0, 0, 0};
   int left = d.ri;
   // a single-component scan is non-interleaved: its MCU is one block, over the
   // component's own block grid (jdinput.c per_scan_setup)
   const bool single = d.nc == 1;
-  const int sbw = single ? (d.c[0].cw + 7) / 8 : 0, sbh = single ? (d.c[0].ch + 7) / 8 : 0;
+  const int cw0 = (d.W * d.c[0].h + d.hmax - 1) / d.hmax, ch0 = (d.H * d.c[0].v + d.vmax - 1) / d.vmax;
+  const int sbw = single ? (cw0 + 7) / 8 : 0, sbh = single ? (ch0 + 7) / 8 : 0;
   const int nmcu = single ? sbw * sbh : mcux * mcuy;
   alignas(16) int16_t blk[64];
   for (int m = 0; m < nmcu; m++) {
@@ -476,10 +484,91 @@ void decode_planes(const uint8_t *b, Dec &d, Scratch &S, int stride[3]) {
               z += 15;
             }
           }
-          idct_ifast(blk, qm[ci], S.plane[ci].data() + (size_t)by * 8 * stride[ci] + bx * 8, stride[ci], T.rl);
+          emit(ci, bx, by, blk);
         }
     }
   }
+}
+
+// Huffman decode + IDCT of the whole scan into the component planes.
+void decode_planes(const uint8_t *b, Dec &d, Scratch &S, int stride[3]) {
+  const Tables &T = tables();
+  int16_t qm[3][64];
+  plane_setup(d, S, stride, qm);
+  decode_scan(b, d, [&](int ci, int bx, int by, const int16_t *blk) {
+    idct_ifast(blk, qm[ci], S.plane[ci].data() + (size_t)by * 8 * stride[ci] + bx * 8, stride[ci], T.rl);
+  });
+}
+
+// TurboJPEG's scaling factors (tjGetScalingFactors, largest first) and
+// tjDecompress2's choice among them: the first whose scaled size fits the
+// requested width x height.
+int tj_scale_choice(int w, int h, uint32_t req_w, uint32_t req_h, int *num, int *den) {
+  static const int sf[16][2] = {{2, 1}, {15, 8}, {7, 4}, {13, 8}, {3, 2}, {11, 8}, {5, 4}, {9, 8},
+                                {1, 1}, {7, 8},  {3, 4}, {5, 8},  {1, 2}, {3, 8},  {1, 4}, {1, 8}};
+  for (int i = 0; i < 16; i++) {
+    const int64_t sw = ((int64_t)w * sf[i][0] + sf[i][1] - 1) / sf[i][1];
+    const int64_t sh = ((int64_t)h * sf[i][0] + sf[i][1] - 1) / sf[i][1];
+    if (sw <= (int64_t)req_w && sh <= (int64_t)req_h) {
+      *num = sf[i][0];
+      *den = sf[i][1];
+      return 0;
+    }
+  }
+  return -1;
+}
+
+// tjTransform(TJXOPT_CROP [+ TJXOP_HFLIP]) (libffcv.cpp:78-98), restated on
+// the decoded coefficients as libjpeg-turbo's transupp.c does it: the crop
+// origin must sit on an iMCU boundary (tjTransform's check); its size is
+// clamped to the image (0 = to the edge; jtransform_request_workspace); the
+// crop is taken in the transformed frame.  do_crop copies blocks; do_flip_h
+// mirrors the whole iMCU columns (block order reversed, odd DCT columns
+// negated) and copies the partial iMCU column at the right edge unchanged.
+// The output image is d's stream with the new size and coefficients, decoded
+// like any other (same tables, colour space and sampling).
+const char *transform_coefs(const uint8_t *b, Dec &d, uint32_t x, uint32_t y, uint32_t w, uint32_t h, bool hflip,
+                            std::vector<int16_t> dst[3]) {
+  const int imw = 8 * d.hmax, imh = 8 * d.vmax;
+  if (x % (uint32_t)imw || y % (uint32_t)imh) return "crop origin is not on an iMCU boundary";
+  if (x >= (uint32_t)d.W || y >= (uint32_t)d.H) return "crop origin outside the image";
+  const int rw = (int)(w == 0 || w > (uint32_t)d.W - x ? (uint32_t)d.W - x : w);
+  const int rh = (int)(h == 0 || h > (uint32_t)d.H - y ? (uint32_t)d.H - y : h);
+  // source coefficients, whole-MCU grids (blocks a non-interleaved scan does not code stay zero)
+  const int mcux = (d.W + imw - 1) / imw, mcuy = (d.H + imh - 1) / imh;
+  std::vector<int16_t> src[3];
+  int sbw[3];
+  for (int i = 0; i < d.nc; i++) {
+    sbw[i] = mcux * d.c[i].h;
+    src[i].assign((size_t)sbw[i] * mcuy * d.c[i].v * 64, 0);
+  }
+  decode_scan(b, d, [&](int ci, int bx, int by, const int16_t *blk) {
+    std::memcpy(src[ci].data() + ((size_t)by * sbw[ci] + bx) * 64, blk, 64 * sizeof(int16_t));
+  });
+  const int W0 = d.W;
+  d.W = rw;
+  d.H = rh;
+  const int dmcux = (rw + imw - 1) / imw, dmcuy = (rh + imh - 1) / imh;
+  for (int i = 0; i < d.nc; i++) {
+    const Comp &c = d.c[i];
+    const int dbw = dmcux * c.h, dbh = dmcuy * c.v;
+    const int wib = (rw * c.h + imw - 1) / imw, hib = (rh * c.v + imh - 1) / imh;  // width/height_in_blocks
+    const int xcb = (int)(x / (uint32_t)imw) * c.h, ycb = (int)(y / (uint32_t)imh) * c.v;
+    const int comp_width = (W0 / imw) * c.h;  // whole iMCU columns (do_flip_h)
+    dst[i].assign((size_t)dbw * dbh * 64, 0);
+    for (int by = 0; by < hib; by++)
+      for (int bx = 0; bx < wib; bx++) {
+        int16_t *o = dst[i].data() + ((size_t)by * dbw + bx) * 64;
+        const int sy = ycb + by;
+        if (hflip && xcb + bx < comp_width) {
+          const int16_t *s = src[i].data() + ((size_t)sy * sbw[i] + (comp_width - xcb - bx - 1)) * 64;
+          for (int k = 0; k < 64; k++) o[k] = (k & 1) ? (int16_t)-s[k] : s[k];
+        } else {
+          std::memcpy(o, src[i].data() + ((size_t)sy * sbw[i] + xcb + bx) * 64, 64 * sizeof(int16_t));
+        }
+      }
+  }
+  return nullptr;
 }
 
 // jdsample.c fancy upsampling of one component row to full width, as ints:
@@ -545,16 +634,9 @@ int imdecode(unsigned char *input_buffer, uint64_t input_size, uint32_t source_h
              uint32_t offset_y, uint32_t scale_num, uint32_t scale_denom, bool enable_crop, bool hflip) {
   (void)source_height;  // unused by the reference too (libffcv.cpp:53-112)
   (void)source_width;
-  (void)offset_x;
-  (void)offset_y;
-  if (!input_buffer || !output_buffer || input_size == 0 || crop_height == 0 || crop_width == 0) {
+  if (!input_buffer || !output_buffer || input_size == 0 || crop_height == 0 || crop_width == 0 || scale_num == 0 ||
+      scale_denom == 0) {
     ffcv::set_error("imdecode: invalid arguments");
-    return -1;
-  }
-  if (enable_crop || hflip || scale_num != scale_denom) {
-    // tjTransform lossless crop / flip and DCT scaling: never used by ffcv
-    // (rgb_image.py:131,196 pass False, False, 1, 1)
-    ffcv::set_error("imdecode: crop / flip / scaling transforms are not supported");
     return -1;
   }
   Dec d;
@@ -562,14 +644,48 @@ int imdecode(unsigned char *input_buffer, uint64_t input_size, uint32_t source_h
     ffcv::set_error("imdecode: %s", err);
     return -1;
   }
-  if ((uint32_t)d.H != crop_height || (uint32_t)d.W != crop_width) {
-    ffcv::set_error("imdecode: requested %ux%u, the JPEG is %dx%d (scaled decoding is not supported)", crop_height,
-                    crop_width, d.H, d.W);
-    return -1;
-  }
   Scratch &S = t_scr;
   int stride[3] = {0, 0, 0};
-  decode_planes(input_buffer, d, S, stride);
+  // libffcv.cpp:95-100: crop (always, with the offsets and size) and the
+  // optional mirror when enable_crop or hflip, else the stream as it is
+  const bool transform = enable_crop || hflip;
+  thread_local std::vector<int16_t> tco[3];
+  if (transform) {
+    if (const char *err = transform_coefs(input_buffer, d, offset_x, offset_y, crop_width, crop_height, hflip, tco)) {
+      ffcv::set_error("imdecode: tjTransform: %s", err);
+      return -1;
+    }
+  }
+  // libffcv.cpp:101-103 tjDecompress2(width = TJSCALED(crop_width, scaling),
+  // height = TJSCALED(crop_height, scaling), pitch 0): TurboJPEG decodes at
+  // the largest of its factors whose output fits; rows are packed at the
+  // decoded width.  Only the factor 1/1 (ifast 8x8) is restated here.
+  const uint32_t req_w = (uint32_t)(((uint64_t)crop_width * scale_num + scale_denom - 1) / scale_denom);
+  const uint32_t req_h = (uint32_t)(((uint64_t)crop_height * scale_num + scale_denom - 1) / scale_denom);
+  int fn = 0, fd = 0;
+  if (tj_scale_choice(d.W, d.H, req_w, req_h, &fn, &fd)) {
+    ffcv::set_error("imdecode: the %dx%d image cannot be scaled into %ux%u", d.H, d.W, req_h, req_w);
+    return -1;
+  }
+  if (fn != fd) {
+    ffcv::set_error("imdecode: the %dx%d image would decode at scale %d/%d into %ux%u (scaled decoding is not "
+                    "supported)", d.H, d.W, fn, fd, req_h, req_w);
+    return -1;
+  }
+  if (transform) {
+    const Tables &T = tables();
+    int16_t qm[3][64];
+    plane_setup(d, S, stride, qm);
+    for (int i = 0; i < d.nc; i++) {
+      const Comp &c = d.c[i];
+      for (int by = 0; by < c.bh; by++)
+        for (int bx = 0; bx < c.bw; bx++)
+          idct_ifast(tco[i].data() + ((size_t)by * c.bw + bx) * 64, qm[i],
+                     S.plane[i].data() + (size_t)by * 8 * stride[i] + bx * 8, stride[i], T.rl);
+    }
+  } else {
+    decode_planes(input_buffer, d, S, stride);
+  }
   const Tables &T = tables();
   const int W = d.W;
   for (int i = 0; i < d.nc; i++) S.row[i].resize((size_t)W);

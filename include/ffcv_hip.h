@@ -133,10 +133,19 @@ void resize(int64_t cresizer, int64_t source_p, int64_t sx, int64_t sy,
  * IDCT, fancy upsampling), on the CPU of the calling thread like the
  * reference (ffcv_cpu_jpeg.hip; thread-safe, per-thread scratch).  Baseline
  * / extended sequential Huffman, 8-bit, 1 or 3 components, restart
- * intervals.  Returns 0, or -1 on a decode error, an unsupported stream
- * (progressive, arithmetic, multi-scan, CMYK), a size other than the image's,
- * or when enable_crop, hflip or a scale other than 1 is requested (never
- * used by ffcv) -- see ffcv_last_error(). */
+ * intervals.  With enable_crop or hflip, the reference's tjTransform
+ * (TJXOPT_CROP at offset_x, offset_y, crop_width x crop_height, plus
+ * TJXOP_HFLIP) is applied to the coefficients first (lossless: the crop origin
+ * must be on an iMCU boundary, the size is clamped to the image, the crop is
+ * taken in the mirrored frame, the partial iMCU column at the right edge is
+ * not mirrored).  As tjDecompress2 does, the decode runs at the largest
+ * TurboJPEG scaling factor whose output fits the requested size (scaled by
+ * scale_num / scale_denom), rows packed at the decoded width; only the
+ * factor 1/1 is restated.  Returns 0, or -1 on a decode error, an
+ * unsupported stream (progressive, arithmetic, multi-scan, CMYK), a
+ * misaligned crop, or a request TurboJPEG would decode at another factor --
+ * see ffcv_last_error().  ffcv itself passes the image's size, 0, 0, 1, 1,
+ * False, False. */
 int imdecode(unsigned char *input_buffer, uint64_t input_size,
              uint32_t source_height, uint32_t source_width,
              unsigned char *output_buffer, uint32_t crop_height,

@@ -108,7 +108,7 @@ def test_host_read_and_imdecode_arguments(tmp_path, hip_lib):
         assert np.array_equal(dst, data[100:400])
     out = np.zeros((8, 8, 3), np.uint8)
     assert L.imdecode(data, out, 8, 8, enable_crop=True) == -1
-    assert b'not supported' in hip_lib.ffcv_last_error()
+    assert b'SOI' in hip_lib.ffcv_last_error()
     assert L.imdecode(data, out, 8, 8, 0, 8) == -1
 
 

@@ -78,8 +78,19 @@ def test_cpu_imdecode_rejects(hip_lib):
     bad[:2] = 0  # no SOI
     assert L.imdecode(bad, out, 40, 56) == -1
     assert b'SOI' in L.lib().ffcv_last_error()
-    assert L.imdecode(blob, np.zeros((41, 56, 3), np.uint8), 41, 56) == -1  # scaled decode
-    assert L.imdecode(blob, out, 40, 56, enable_crop=True) == -1
+    # tjDecompress2 decodes at the largest scaling factor that fits the
+    # request: 41 x 56 fits only 1/1 (rows packed at the image's width) ...
+    big = np.full((41, 56, 3), 7, np.uint8)
+    assert L.imdecode(blob, big, 40, 56, 41, 56) == 0
+    assert np.array_equal(big[:40], out) and (big[40] == 7).all()
+    # ... 45 x 63 fits 9/8, a scaled decode this restatement does not do
+    assert L.imdecode(blob, np.zeros((45, 63, 3), np.uint8), 40, 56, 45, 63) == -1
+    assert b'scale 9/8' in L.lib().ffcv_last_error()
+    assert L.imdecode(blob, out, 40, 56, 40, 56, 0, 0, 1, 2) == -1  # 1/2: reduced IDCT, not restated
+    # the lossless crop's origin must be on an iMCU boundary (16 x 16 at 4:2:0)
+    assert L.imdecode(blob, out, 40, 56, 24, 24, 8, 0, enable_crop=True) == -1
+    assert b'iMCU' in L.lib().ffcv_last_error()
+    assert L.imdecode(blob, out, 40, 56, 8, 8, 64, 0, enable_crop=True) == -1  # origin outside
     prog = _pil(img, quality=90, progressive=True)
     assert L.imdecode(prog, out, 40, 56) == -1
     assert b'progressive' in L.lib().ffcv_last_error()
@@ -104,6 +115,52 @@ def test_cpu_imdecode_rejects(hip_lib):
     frac[sof + 4] = 0x21
     assert L.imdecode(np.frombuffer(bytes(frac), np.uint8), out, 40, 56) == -1
     assert b'sampling' in L.lib().ffcv_last_error()
+
+
+def test_cpu_imdecode_transform(hip_lib):
+    """libffcv.cpp:78-103: tjTransform(TJXOPT_CROP [+ TJXOP_HFLIP]) then
+    tjDecompress2, restated on the coefficients (transupp.c do_crop /
+    do_flip_h).  Parity unpinned: libturbojpeg (the transform) is not in this
+    image, only Pillow's libjpeg; these are the properties the lossless
+    transforms guarantee."""
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(8)
+
+    def dec(blob, h, w, ch, cw, ox=0, oy=0, crop=False, flip=False):
+        out = np.full((ch, cw, 3), 3, np.uint8)
+        rc = L.imdecode(blob, out, h, w, ch, cw, ox, oy, 1, 1, crop, flip)
+        assert rc == 0, L.lib().ffcv_last_error()
+        return out
+
+    # the full image as the crop: the same coefficients, the same pixels
+    img = natural_image(rng, 72, 100)
+    b420 = _pil(img, quality=90, subsampling=2)
+    full = dec(b420, 72, 100, 72, 100)
+    assert np.array_equal(dec(b420, 72, 100, 72, 100, crop=True), full)
+    # 4:4:4 (no upsampling): a block-aligned crop is exactly the crop of the decode
+    b444 = _pil(img, quality=90, subsampling=0)
+    f444 = dec(b444, 72, 100, 72, 100)
+    assert np.array_equal(dec(b444, 72, 100, 24, 40, 16, 8, crop=True), f444[8:32, 16:56])
+    # clamped to the image (TJ: r.w past the edge -> to the edge), rows packed at the clamped width
+    c = dec(b444, 72, 100, 20, 56, 48, 56, crop=True)  # real 16 x 52 (9/8 would need 18 x 59)
+    assert np.array_equal(c.reshape(-1)[:16 * 52 * 3].reshape(16, 52, 3), f444[56:, 48:])
+    # 4:2:0: away from the crop's borders the fancy upsampling sees the same chroma
+    c = dec(b420, 72, 100, 40, 48, 32, 16, crop=True)
+    assert np.array_equal(c[2:-2, 2:-2], full[18:54, 34:78])
+    # horizontal mirror, grey, width 8k + 3: the whole blocks are mirrored (odd
+    # DCT columns negated: the same pixels up to the IDCT's rounding), the
+    # partial block at the right edge stays where it is, unchanged
+    g = natural_image(rng, 40, 67)[:, :, 0].copy()
+    bg = _pil(g, quality=90)
+    fg = dec(bg, 40, 67, 40, 67)
+    fl = dec(bg, 40, 67, 40, 67, flip=True)
+    assert np.array_equal(fl[:, 64:], fg[:, 64:])
+    d = np.abs(fl[:, :64].astype(int) - fg[:, 63::-1].astype(int))
+    assert d.max() <= 2 and d.mean() < 0.5, (d.max(), d.mean())
+    # the crop is taken in the mirrored frame: columns [8, 24) of the mirror
+    assert np.array_equal(dec(bg, 40, 67, 16, 16, 8, 8, crop=True, flip=True), fl[8:24, 8:24])
+    # hflip alone still crops with the given offsets and size (libffcv.cpp:89-93)
+    assert np.array_equal(dec(bg, 40, 67, 16, 24, 16, 8, flip=True), fl[8:24, 16:40])
 
 
 def test_cpu_decode_batch(hip_lib, oracle):

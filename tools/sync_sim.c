@@ -404,6 +404,85 @@ int main(int argc, char **argv) {
            (double)bs_sum / nsamp, (double)ps_sum / nsamp, ps_max, bpm, (double)best_sum / nsamp);
     return 0;
   }
+  if (heur == 11) {  // write-pass split: lane ranges vs pieces of the prefix up to the
+                     // block that starts MCU row SIM_ROWF * rows, cut at converged states
+                     // (lane starts + the first NEV block starts on the 2^sh grid)
+    double rowf = getenv("SIM_ROWF") ? atof(getenv("SIM_ROWF")) : 0.85;
+    int NEVS = 6;
+    uint32_t *sympos = malloc(sizeof(uint32_t) * (tbits + 2));  // symbols started before bit b
+    uint32_t *bstart = malloc(sizeof(uint32_t) * (tbits / 6 + 16));
+    int *bz = malloc(sizeof(int) * (tbits + 2));
+    long nb = 0, ns = 0;
+    uint32_t pos = 0;
+    int z = 0, ph = 0;
+    for (uint32_t b = 0; b <= tbits; b++) { sympos[b] = 0; bz[b] = -1; }
+    while (pos < tbits) {
+      bz[pos] = z;
+      if (z == 0) bstart[nb++] = pos;
+      int len, bad, ti = z == 0 ? ph_dc[ph] : ph_ac[ph];
+      int v = sym(ti, pos, &len, &bad);
+      int sz = z == 0 ? v : (v & 15), r = z == 0 ? 0 : v >> 4;
+      uint32_t np = pos + len + sz;
+      for (uint32_t b = pos + 1; b <= np && b <= tbits; b++) sympos[b] = ns + 1;
+      ns++;
+      pos = np;
+      int zac = sz ? z + r + 1 : (r == 15 ? z + 16 : 64);
+      z = z == 0 ? 1 : zac;
+      if (z >= 64) { z = 0; ph = (ph + 1) % bpm; }
+    }
+    for (uint32_t b = pos; b <= tbits; b++) sympos[b] = ns;
+    uint32_t cbits = (tbits + lanes - 1) / lanes;
+    // lane starts: first symbol boundary >= t * cbits; its first block start; events
+    uint32_t *ls = malloc(sizeof(uint32_t) * (lanes + 1));
+    long *lb = malloc(sizeof(long) * (lanes + 1));
+    uint32_t cand[4096];
+    long candb[4096];
+    int nc = 0;
+    long bi = 0;
+    double evq = ((double)nb / lanes + NEVS) / NEVS;
+    int sh = 0;
+    while ((1 << sh) < (int)evq) sh++;
+    for (int t = 0; t < lanes; t++) {
+      uint32_t p0 = t * cbits;
+      while (p0 < tbits && bz[p0] < 0) p0++;
+      ls[t] = p0;
+      while (bi < nb && bstart[bi] < p0) bi++;
+      lb[t] = bi;  // first block started at or after the lane start
+      cand[nc] = p0;
+      candb[nc++] = bz[p0] == 0 ? bi : -1;
+      uint32_t end = (t + 1) * cbits;
+      for (int q = 0; q < NEVS; q++) {
+        long bq = bi + ((long)q << sh);
+        if (bq < nb && bstart[bq] < end && bstart[bq] > p0) { cand[nc] = bstart[bq]; candb[nc++] = bq; }
+      }
+    }
+    long need = (long)(rowf * nb);
+    uint32_t E = tbits;
+    for (int c = 0; c < nc; c++)
+      if (candb[c] >= need) { E = cand[c]; break; }
+    long base_max = 0, new_max = 0;
+    for (int t = 0; t < lanes; t++) {
+      uint32_t a = t * cbits, b = t == lanes - 1 ? tbits : (t + 1) * cbits;
+      long s = (long)sympos[b < tbits ? b : tbits] - sympos[a < tbits ? a : tbits];
+      if (s > base_max) base_max = s;
+    }
+    uint32_t *pc = malloc(sizeof(uint32_t) * (lanes + 1));
+    for (int i = 0; i < lanes; i++) {
+      uint32_t tg = (uint32_t)((uint64_t)i * E / lanes);
+      uint32_t c0 = E;
+      for (int c = 0; c < nc; c++)
+        if (cand[c] >= tg) { c0 = cand[c]; break; }
+      pc[i] = c0 < E ? c0 : E;
+    }
+    pc[lanes] = E;
+    for (int i = 0; i < lanes; i++) {
+      long s = pc[i + 1] > pc[i] ? (long)sympos[pc[i + 1]] - sympos[pc[i]] : 0;
+      if (s > new_max) new_max = s;
+    }
+    printf("blocks %ld symbols %ld sh %d | E/total %.3f | lane-range max symbols %ld | piece max %ld (%.3f)\n", nb, ns,
+           sh, (double)E / tbits, base_max, new_max, (double)new_max / base_max);
+    return 0;
+  }
   uint32_t cb = (tbits + lanes - 1) / lanes;
   Traj *T = calloc(lanes, sizeof(Traj));
   St *g = calloc(lanes, sizeof(St));

@@ -15,7 +15,9 @@ which lowers to three kernels per launch: jpeg_entropy_kernel<RRC> (K1:
 descriptor gather, crop/cutout draws, parse, de-stuff, parallel Huffman
 decode of the crop's coefficients), jpeg_idct_kernel (K1b: DC prediction,
 dequantise + ifast IDCT of the crop's blocks) and jpeg_color_resize_kernel
-(K2: upsample + colour, INTER_AREA, cutout, LUT).  The 1.28M-entry dataset
+(K2: upsample + colour, INTER_AREA, cutout, LUT; one workgroup per 16-row
+band, or jpeg_rrc_loop_kernel, seven bands per workgroup, for launches of
+>= 8,192 images).  The 1.28M-entry dataset
 is built from U unique encodings replicated at distinct HBM addresses.
 
 After the timed region (outside it) the rows each slot's last timed launch
@@ -737,24 +739,32 @@ def main():
     k2 = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>' if k2_loop else
           f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
     kernels = ['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', k2] if mode == 'jpg' else ['rrc_raw_kernel<false>']
+    # the timed launches' own K2 (the driver's 20 steps: launches of 2,048-4,096
+    # images, the per-band kernel) for the whole-path figures (path, traffic)
+    k2t = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>'
+           if max(launch_imgs) >= k2_min and not args.k2flags else
+           f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
+    timed_kernels = kernels[:2] + [k2t] if mode == 'jpg' else kernels
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
     # (tools/profile.sh -> tools/pmc_summary.py): bytes per image x images per launch
     pm = load_profile(f'traffic_{args.config}.json')
+    if pm and not all(n in pm for n in timed_kernels):
+        timed_kernels = kernels
     if pm and all(n in pm and 'fetch_size_kb' in pm[n] and 'write_size_kb' in pm[n] and 'images' in pm[n]
-                  for n in kernels):
+                  for n in timed_kernels):
         # gfx950 FETCH_SIZE counts 64 B per 128-B request of 16-byte-per-lane
         # streaming loads (MI355X_MICROARCH.md, HBM): the raw kernel stages
         # with uint4 loads, so its fetch counts half its bytes
-        fx = {n: 2.0 if n.startswith('rrc_raw_kernel') else 1.0 for n in kernels}
+        fx = {n: 2.0 if n.startswith('rrc_raw_kernel') else 1.0 for n in timed_kernels}
         per_img = sum((pm[n]['fetch_size_kb'] * fx[n] + pm[n]['write_size_kb']) * 1024.0 / pm[n]['images']
-                      for n in kernels)
+                      for n in timed_kernels)
         hbm['traffic'] = round(per_img * imgs_per_launch, 1)
         hbm['traffic_per_image'] = round(per_img, 1)
         hbm['traffic_note'] = (f'HBM bytes per launch of {imgs_per_launch:.0f} images (FETCH_SIZE'
                                f'{" x2 (16-B loads, gfx950)" if mode != "jpg" else ""} + WRITE_SIZE, '
                                f'rocprofv3 PMC, profiles/traffic_{args.config}.json, build {pm.get("_build")}); '
                                f'algorithmic {unit_bytes * imgs_per_launch:.0f}')
-    launch = {'kernel': ' + '.join(kernels) + f' (launches of {imgs_per_launch:.0f} images)',
+    launch = {'kernel': ' + '.join(timed_kernels) + f' (launches of {imgs_per_launch:.0f} images)',
               'launches': n_launch, 'launch_ms': round(eff_launch_ms, 4),
               'launch_ms_events': round(float(np.mean(launch_ms)), 4)}
     roof = dict(hbm, **launch)
@@ -782,13 +792,14 @@ def main():
     if mode == 'jpg' and sq and all(n in sq for n in kernels):
         # the JPEG path is bound by instruction issue / latency of the serial
         # Huffman chain, not HBM: VALU wave-instructions per
-        # image (SQ_INSTS_VALU, rocprofv3) x images/s
-        valu_img = sum(sq[n]['valu_per_image'] for n in kernels)
+        # image (SQ_INSTS_VALU, rocprofv3) of the timed launches' kernels x images/s
+        pk = timed_kernels if all(n in sq for n in timed_kernels) else kernels
+        valu_img = sum(sq[n]['valu_per_image'] for n in pk)
         issue = valu_img * per_gpu_rate / 1e9
         roof = {'bound': 'issue', 'achieved': round(issue, 2), 'peak': VALU_PEAK_GIPS,
                 'unit': 'G VALU wave-instr/s', 'frac': round(issue / VALU_PEAK_GIPS, 4),
                 'traffic': hbm['traffic'], **launch,
-                'valu_per_image': {n: round(sq[n]['valu_per_image'], 1) for n in kernels},
+                'valu_per_image': {n: round(sq[n]['valu_per_image'], 1) for n in pk},
                 'note': (f'SQ_INSTS_VALU per image from profiles/sq_{args.config}.json (rocprofv3 --pmc, build '
                          f'{sq.get("_build")}) x images/s; peak = 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 '
                          f'VALU instruction (the measured issue rate of the integer VOP3 forms, '

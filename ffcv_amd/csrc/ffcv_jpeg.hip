@@ -462,7 +462,11 @@ FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 
 // that absorbs every non-recording store).  With use_old (a later round) it
 // stops at a block start that matches an event of the lane's previous
 // trajectory and splices onto it: from an identical state the old trajectory
-// is exact, so its remaining count and exit state are reused.  The old-event
+// is exact, so its remaining count and exit state are reused.  A splice off
+// the new trajectory's slot grid keeps the old events from the hit on, on a
+// grid based at the hit's block count (eb), when they outnumber the new ones:
+// a lane re-run again in a later round then still finds them (the sync
+// rounds' wave-iterations fell 808 -> 774 per image, round 4).  The old-event
 // cursor advances one event per symbol (old events behind the decode
 // position can never match); lagging only delays a splice, never makes a
 // wrong one.  Events are double-buffered: buffer cb holds the previous
@@ -474,9 +478,9 @@ FFCV_DEV int slot_of(uint32_t pack, int ph) { return (int)((pack >> (3 * ph)) & 
 // the top of the step (next phase's table infos, next old event).
 template <bool use_old, class TB>
 FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, DecState st,
-                             uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, DecState old_exit,
-                             int sh, uint32_t &iters) {
-  const int smask = (1 << sh) - 1;  // events: every 2^sh-th block start (slot q = block q << sh)
+                             uint32_t end_bit, int lane, uint32_t &cnt, int &nev, int &cb, int &eb,
+                             DecState old_exit, int sh, uint32_t &iters) {
+  const int smask = (1 << sh) - 1;  // events: every 2^sh-th block start (slot q = block eb + (q << sh))
   BitReader br;
   br.init(words, st.pos);
   uint32_t pos = st.pos;
@@ -527,20 +531,30 @@ FFCV_DEV DecState sync_range(JShared &S, const TB &T, const uint32_t *words, Dec
     dinf = bend ? ndinf : dinf;
     ainf = bend ? nainf : ainf;
   }
-  if (hit) {  // at the previous trajectory's event j = its block start j << sh
+  if (hit) {  // at the previous trajectory's event j = its block start eb + (j << sh)
+    const uint32_t ocnt = (uint32_t)eb + ((uint32_t)j << sh);
     int m = min((n + smask) >> sh, NEV);  // slots written so far
     if ((n & smask) == 0 && m < NEV) {     // the old events stay on the slot grid: keep them
       const int keep = min(onev - j, NEV - m);
       for (int q = 0; q < keep; q++) evn[(m + q) * JL] = evo[(j + q) * JL];
       m += keep;
+      eb = 0;
+    } else if (onev - j > m) {  // off the grid: the old events from j on, on a grid based at n
+      const int keep = min(onev - j, NEV);
+      for (int q = 0; q < keep; q++) evn[q * JL] = evo[(j + q) * JL];
+      m = keep;
+      eb = n;
+    } else {
+      eb = 0;
     }
     nev = m;
-    cnt = (uint32_t)n + (cnt - ((uint32_t)j << sh));
+    cnt = (uint32_t)n + (cnt - ocnt);
     cb = nbuf;
     return old_exit;
   }
   nev = min((n + smask) >> sh, NEV);
   cnt = (uint32_t)n;
+  eb = 0;
   cb = nbuf;
   DecState out;
   out.pos = pos;
@@ -1422,13 +1436,13 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
   g.z = 0;
   g.ph = 0;
   uint32_t my_cnt = 0;
-  int my_nev = 0, my_cb = 0;
+  int my_nev = 0, my_cb = 0, my_eb = 0;  // events: count, buffer, block count of slot 0
   DecState e = g;
   uint32_t it_lane = 0, it_wave = 0;  // diagnostics: loop iterations (max over lanes per round)
   // event stride: NEV events spread over a lane's expected block count
   const uint32_t evq = ((uint32_t)S.nblocks / nthr + NEV) / NEV;
   const int esh = evq <= 1 ? 0 : 32 - __clz((int)(evq - 1));
-  if (active) e = sync_range<false>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, g, esh, it_lane);
+  if (active) e = sync_range<false>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, my_eb, g, esh, it_lane);
   if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
   int rounds = 0;
   for (;;) {
@@ -1445,9 +1459,10 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
         e = g;
         my_cnt = 0;
         my_nev = 0;
+        my_eb = 0;
       } else {
         it_lane = 0;
-        e = sync_range<true>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, e, esh, it_lane);
+        e = sync_range<true>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, my_eb, e, esh, it_lane);
       }
     }
     if (a.dbg) it_wave += __reduce_max_sync(~0ull, changed ? it_lane : 0u);
@@ -1521,6 +1536,15 @@ FFCV_DEV int alloc_scratch(JShared &S, const JpegArgs &a, uint32_t nbytes, int t
   const uint64_t dc = MODE == JM_COEF ? align256((uint64_t)S.nblocks * 2) : 0, pl = align256((uint64_t)S.nwin * 64);
   const uint64_t rgb = MODE == JM_RRC ? align256((uint64_t)S.rh * S.rw * 3) : 0;
   const uint64_t need = ds + cf + dc + pl + rgb;
+  // An image larger than the whole arena reserves nothing (a 2400x1800 image
+  // decoded first, largest-first, would otherwise hold the arena whenever its
+  // give-back below loses the race, failing every image of the launch).  A
+  // check against the live counter measured -1.5% (one more memory round
+  // trip before the workgroup barrier).
+  if (need > a.arena_bytes) {
+    if (t == 0) a.info[k].arena_need = 0;
+    return FFCV_SAMPLE_TOO_LARGE;
+  }
   unsigned long long base = 0;
   if (t == 0) base = atomicAdd(a.arena_top, (unsigned long long)need);
   // readfirstlane returns int: widen through uint32_t (an offset at or past

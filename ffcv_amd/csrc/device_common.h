@@ -219,12 +219,16 @@ FFCV_HD void center_crop(uint32_t height, uint32_t width, double ratio, int32_t 
 // Returns 1 when the MT19937 stream ran out (FFCV_SAMPLE_RNG).
 FFCV_HD int draw_part(int part, int k, uint64_t id, uint32_t H, uint32_t W, const ffcv_draw_params &p,
                        int32_t *crops, int32_t *cut, uint8_t *flips) {
+  // Each part's stream is seeded before the per-part branches (op id = part
+  // + 1): the entropy kernel draws a sample's three parts on three lanes side
+  // by side, which then run the 397-step seeding chain once, together,
+  // instead of once per branch (three serial chains at every workgroup start)
   DevMT m;
+  mt_init(m, sample_seed(p.loader_seed, p.epoch, id, (uint32_t)part + 1));
   if (part == 0 && crops) {
     int32_t c[4];
     int err = 0;
     if (p.crop_kind == 0) {
-      mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 1));
       random_crop(m, H, W, p.scale, p.ratio, c);
       err = m.err;
     } else {
@@ -237,13 +241,11 @@ FFCV_HD int draw_part(int part, int k, uint64_t id, uint32_t H, uint32_t W, cons
     return err;
   }
   if (part == 1 && cut && p.cutout_size > 0) {
-    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 2));
     cut[2 * k + 0] = (int32_t)mt_randint(m, p.out_h - p.cutout_size + 1);
     cut[2 * k + 1] = (int32_t)mt_randint(m, p.out_w - p.cutout_size + 1);
     return m.err;
   }
   if (part == 2 && flips) {
-    mt_init(m, sample_seed(p.loader_seed, p.epoch, id, 3));
     flips[k] = (uint8_t)(mt_double(m) < p.flip_prob);
   }
   return 0;

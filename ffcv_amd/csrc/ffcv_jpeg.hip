@@ -1820,6 +1820,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const uint64_t cf_off = ((uint64_t)wuni((uint32_t)(S.cf_off >> 32)) << 32) | wuni((uint32_t)S.cf_off);
   int16_t *coef = (int16_t *)(a.arena + cf_off);
 
+#if defined(K1_STOP) && K1_STOP == 1  // timing only: K1 up to the tables (no de-stuff)
+  if (cf_off != 0x7fffffffffffull) return;
+#endif
   // ------------------------------------------------------------- P2 ----
   // De-stuffing in stream order: each step the wave reads 64 consecutive
   // aligned dwords of the segment (one per lane), keeps every byte except a

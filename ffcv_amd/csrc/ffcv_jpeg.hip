@@ -1866,65 +1866,83 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     // load unconditionally and the compiler can count vmcnt statically
     const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc((void *)wave_uniform(aw), 0, (int)(ndw * 4), BUF_CFG);
     auto ld = [&](uint32_t d) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(srs, d * 4, 0, 0); };
-    uint32_t r[DS_DEPTH];
+    // Each lane takes two consecutive dwords per step (8 bytes): the step's
+    // fixed work -- the wave scan of the kept counts, the neighbour bytes,
+    // the marker ballot, the ring bookkeeping -- is shared by twice the bytes.
+    // Byte masks stay in 0x80-per-byte form (zm), so no multiply gathers bits.
+    constexpr int D2 = DS_DEPTH / 2;  // ring depth in two-dword lane steps
+    static_assert(DS_FLUSH == DS_DEPTH, "one flush per ring cycle");
+    uint32_t r0[D2], r1[D2];
 #pragma unroll
-    for (int u = 0; u < DS_DEPTH; u++) r[u] = ld(u * JL + t);
-    int step = 0;
+    for (int u = 0; u < D2; u++) {
+      r0[u] = ld(2 * (u * JL + t));
+      r1[u] = ld(2 * (u * JL + t) + 1);
+    }
     bool done = false;
-    for (uint32_t base4 = 0; !done; base4 += DS_DEPTH * JL) {
+    auto zm = [](uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
+    // kept / marker bytes of one dword (0x80 per byte) at stream index rel0 of its byte 0
+    auto scan_dw = [&](uint32_t w, uint32_t prevb, uint32_t nextb, int rel0, uint32_t &keep, uint32_t &mark) {
+      const uint32_t pw = (w << 8) | prevb;          // previous byte of each byte
+      const uint32_t nw = (w >> 8) | (nextb << 24);  // next byte of each byte
+      const int lo = max(0, -rel0), hi = min(4, (int)seglen - rel0);  // valid bytes [lo, hi)
+      const uint32_t vhi = hi >= 4 ? 0x80808080u : (hi <= 0 ? 0u : 0x80808080u >> (32 - 8 * hi));
+      const uint32_t valid = vhi & (0x80808080u << (8 * lo));
+      const uint32_t ff = zm(~w);
+      // a 0x00 after 0xFF is stuffing, except the segment's first byte
+      const uint32_t head = rel0 <= 0 ? 0x80808080u >> (24 - 8 * min(3, -rel0)) : 0u;  // bytes with rel <= 0
+      const uint32_t removed = zm(w) & zm(~pw) & ~head;
+      // a marker is 0xFF followed by a non-zero byte; end of data acts as one
+      const uint32_t lastm = (hi >= 1 && rel0 + hi == (int)seglen) ? 0x80u << (8 * (hi - 1)) : 0u;
+      mark = ((ff & ~zm(nw)) | (ff & lastm)) & valid;
+      keep = valid & ~removed;
+    };
+    for (uint32_t base2 = 0; !done; base2 += D2 * JL) {
 #pragma unroll
-      for (int u = 0; u < DS_DEPTH; u++) {
-        const uint32_t base = base4 + u * JL;
-        const uint32_t w = r[u];
-        r[u] = ld(base + DS_DEPTH * JL + t);  // issued on every step (see srs)
-        if (done || base >= ndw) {
+      for (int u = 0; u < D2; u++) {
+        const uint32_t base = base2 + u * JL;  // two-dword lane step of lane 0
+        const uint32_t w0 = r0[u], w1 = r1[u];
+        const uint32_t nd = 2 * (base + D2 * JL + t);
+        r0[u] = ld(nd);  // issued on every step (see srs)
+        r1[u] = ld(nd + 1);
+        if (done || 2 * base >= ndw) {
           done = true;
           continue;
         }
-        const uint32_t di = base + t;
-        const uint32_t wprev = lane_prev(w);
-        const uint32_t wnext = lane_next(w);
-        const uint32_t nfirst = seg_read(r[(u + 1) % DS_DEPTH], 0, sg);  // next step's first dword
-        const uint32_t prevb = t == 0 ? carry : (wprev >> 24);
-        const uint32_t next0 = (t == JL - 1 ? nfirst : wnext) & 0xff;
-        // SWAR over the 4 bytes (byte j = stream byte 4*di + j - mis):
-        // zm(x) has 0x80 in every byte of x that is zero
-        auto zm = [](uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
-        auto bits4 = [](uint32_t m80) { return (((m80 >> 7) & 0x01010101u) * 0x01020408u) >> 24; };
-        const uint32_t pw = (w << 8) | prevb;          // previous byte of each byte
-        const uint32_t nw = (w >> 8) | (next0 << 24);  // next byte of each byte
-        const int rel0 = (int)(4 * di) - (int)mis;     // stream index of byte 0
-        const int lo = max(0, -rel0), hi = min(4, (int)seglen - rel0);  // valid bytes [lo, hi)
-        const uint32_t valid4 = hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
-        const uint32_t ff = zm(~w);
-        // a 0x00 after 0xFF is stuffing, except the segment's first byte
-        const uint32_t head = rel0 <= 0 ? (2u << min(3, -rel0)) - 1u : 0u;  // bytes with rel <= 0
-        const uint32_t removed4 = bits4(zm(w) & zm(~pw)) & ~head;
-        // a marker is 0xFF followed by a non-zero byte; end of data acts as one
-        const uint32_t lastm = (hi >= 1 && hi <= 4 && rel0 + hi == (int)seglen) ? 1u << (hi - 1) : 0u;
-        const uint32_t mark4 = (bits4(ff & ~zm(nw)) | (bits4(ff) & lastm)) & valid4;
-        const int first_mk = mark4 ? __builtin_ctz(mark4) : 4;
-        uint32_t keepm = valid4 & ~removed4 & ((1u << first_mk) - 1u);
-        // the first marker of the step ends the segment
-        const uint64_t mk = seg_ballot(first_mk < 4, sg);
+        const uint32_t d0 = 2 * (base + t);
+        const uint32_t w1prev = lane_prev(w1);
+        const uint32_t w0next = lane_next(w0);
+        const uint32_t nfirst = seg_read(r0[(u + 1) % D2], 0, sg);  // next step's first dword
+        const uint32_t prevb = t == 0 ? carry : (w1prev >> 24);
+        const uint32_t next1 = (t == JL - 1 ? nfirst : w0next) & 0xff;
+        const int rel0 = (int)(4 * d0) - (int)mis;  // stream index of w0's byte 0
+        uint32_t k0, m0, k1, m1;
+        scan_dw(w0, prevb, w1 & 0xff, rel0, k0, m0);
+        scan_dw(w1, w0 >> 24, next1, rel0 + 4, k1, m1);
+        // the first marker of the step ends the segment: keep the bytes before it
+        const uint32_t b0 = m0 ? (m0 & (0u - m0)) - 1u : 0xffffffffu;
+        const uint32_t b1 = m0 ? 0u : (m1 ? (m1 & (0u - m1)) - 1u : 0xffffffffu);
+        k0 &= b0;
+        k1 &= b1;
+        const uint64_t mk = seg_ballot((m0 | m1) != 0, sg);
         if (mk) {
           const int ml = __ffsll((unsigned long long)mk) - 1;
-          if (t > ml) keepm = 0;
+          if (t > ml) k0 = k1 = 0;
           done = true;
         }
-        const uint32_t cnt = __popc(keepm);
-        uint32_t off = dlen + seg_exscan(cnt) - fbase;
+        const uint32_t c0 = __popc(k0), cnt = c0 + __popc(k1);
+        const uint32_t off = dlen + seg_exscan(cnt) - fbase;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {  // branch-free: dropped bytes go to a dummy byte
-          const bool kj = (keepm >> j) & 1;
-          S.stage[kj ? off + __popc(keepm & ((1u << j) - 1u)) : STAGE_DUMMY] = (uint8_t)(w >> (8 * j));
+        for (int j = 0; j < 8; j++) {  // branch-free: dropped bytes go to a dummy byte
+          const uint32_t km = j < 4 ? k0 : k1, w = j < 4 ? w0 : w1;
+          const int jj = j & 3;
+          const bool kj = (km >> (8 * jj + 7)) & 1;
+          const uint32_t before = (j < 4 ? 0u : c0) + (jj ? __popc(km & ((1u << (8 * jj)) - 1u)) : 0u);
+          S.stage[kj ? off + before : STAGE_DUMMY] = (uint8_t)(w >> (8 * jj));
         }
-        off += cnt;
-        dlen = seg_read(off, JL - 1, sg) + fbase;
-        carry = seg_read(w, JL - 1, sg) >> 24;
+        dlen = seg_read(off + cnt, JL - 1, sg) + fbase;
+        carry = seg_read(w1, JL - 1, sg) >> 24;
       }
-      if (!done && (step += DS_DEPTH) == DS_FLUSH) {  // flush whole dwords, keep the 0..3-byte tail
-        step = 0;
+      if (!done) {  // flush whole dwords, keep the 0..3-byte tail
         const uint32_t upto = dlen & ~3u;
         flush(upto);
         if (t < (int)(dlen - upto)) S.stage[t] = S.stage[upto - fbase + t];

@@ -1737,6 +1737,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   }
   wsync_lds();
   STAMP(10);
+#if defined(K1_STOP) && K1_STOP == 7  // timing only: gather, draws and header staging
+  if (smp.size != 0x7fffffffffffull) return;
+#endif
   if (t == 0) S.src = src;
   if (JL == JT || t == 0) {  // the whole wave runs the (scalar) parse; see parse_header
     int st = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, wave_uniform(src), nbytes, smp, a, k, MODE)) : -1;
@@ -1745,6 +1748,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   }
   __syncthreads();
 
+#if defined(K1_STOP) && K1_STOP == 8  // timing only: up to the parse and the scratch allocation
+  if (smp.size != 0x7fffffffffffull) return;
+#endif
   // ------------------------------------------------------------- P1 ----
   // The workgroup's first valid image provides the shared tables; every
   // image whose table slots and DHT bytes equal that image's uses them.

@@ -8,6 +8,9 @@ TAG=${1:-k1v}
 VARS=${2:-"stop2 stop4 stop5 full"}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# generate (and cache in /tmp) the samples outside the profiler: a worker pool
+# forked under rocprofv3 hung at its end on a fresh box
+timeout -k 10 600 python3 -c "import bench; bench.make_unique('jpg', 256, 65536, 0, 16)" || exit 1
 for v in $VARS; do
   lib="--lib build/ab/$v.so"; [ $v = full ] && lib=""
   timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d gpurun_out/${TAG}_$v -o run -- python3 bench.py $lib --only 1 --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches --no-host-check --no-later-epochs --no-c5 --parity-rows 0 --no-kernel-events > gpurun_out/${TAG}_$v.log 2>&1 || { tail -3 gpurun_out/${TAG}_$v.log; exit 1; }

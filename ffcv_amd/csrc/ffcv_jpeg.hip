@@ -974,6 +974,14 @@ FFCV_DEV uint32_t wuni(uint32_t v) {
 // wave every lane runs it on wave-uniform (scalar) values: each byte read is
 // broadcast to a scalar register, so the walk's branches and arithmetic are
 // scalar instead of one lane under an exec mask.
+// x / d for x >= 0 and a sampling factor or ratio d in 1..4 (the parse
+// rejects anything else): shifts, or a multiply-high for 3, instead of a
+// ~25-instruction VALU division sequence (the operands are wave-uniform, so
+// these stay on the scalar unit)
+FFCV_DEV int dsmall(int x, int d) {
+  return d == 3 ? (int)(((uint64_t)(uint32_t)x * 0xAAAAAAABull) >> 33) : x >> (d >> 1);
+}
+
 FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const ffcv_sample &smp_in,
                           const JpegArgs &a, int k_in, int MODE) {
   nbytes = wuni(nbytes);
@@ -1156,8 +1164,8 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     S.color_rgb = 0;
   }
   if (S.ncomp == 1) {
-    S.cw[0] = (S.W * S.hs[0] + S.hmax - 1) / S.hmax;
-    S.ch[0] = (S.H * S.vs[0] + S.vmax - 1) / S.vmax;
+    S.cw[0] = dsmall(S.W * S.hs[0] + S.hmax - 1, S.hmax);
+    S.ch[0] = dsmall(S.H * S.vs[0] + S.vmax - 1, S.vmax);
     S.mcux = (S.cw[0] + 7) / 8;
     S.mcuy = (S.ch[0] + 7) / 8;
     S.bw[0] = S.mcux;
@@ -1165,11 +1173,11 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     S.hs[0] = S.vs[0] = 1;  // non-interleaved scan: one block per MCU
     S.hmax = S.vmax = 1;
   } else {
-    S.mcux = (S.W + 8 * S.hmax - 1) / (8 * S.hmax);
-    S.mcuy = (S.H + 8 * S.vmax - 1) / (8 * S.vmax);
+    S.mcux = dsmall((S.W + 8 * S.hmax - 1) >> 3, S.hmax);
+    S.mcuy = dsmall((S.H + 8 * S.vmax - 1) >> 3, S.vmax);
     for (int c = 0; c < S.ncomp; c++) {
-      S.cw[c] = (S.W * S.hs[c] + S.hmax - 1) / S.hmax;
-      S.ch[c] = (S.H * S.vs[c] + S.vmax - 1) / S.vmax;
+      S.cw[c] = dsmall(S.W * S.hs[c] + S.hmax - 1, S.hmax);
+      S.ch[c] = dsmall(S.H * S.vs[c] + S.vmax - 1, S.vmax);
       S.bw[c] = S.mcux * S.hs[c];
       S.bh[c] = S.mcuy * S.vs[c];
     }
@@ -1195,9 +1203,9 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
     S.rw = S.W;
   }
   for (int c = 0; c < S.ncomp; c++) {  // blocks the crop reads (+1 sample of fancy context)
-    int he = S.hmax / S.hs[c], ve = S.vmax / S.vs[c];
-    int y0 = S.ri / ve - (ve == 2 ? 1 : 0), y1 = (S.ri + S.rh - 1) / ve + (ve == 2 ? 1 : 0);
-    int x0 = S.rj / he - (he == 2 ? 1 : 0), x1 = (S.rj + S.rw - 1) / he + (he == 2 ? 1 : 0);
+    int he = dsmall(S.hmax, S.hs[c]), ve = dsmall(S.vmax, S.vs[c]);
+    int y0 = dsmall(S.ri, ve) - (ve == 2 ? 1 : 0), y1 = dsmall(S.ri + S.rh - 1, ve) + (ve == 2 ? 1 : 0);
+    int x0 = dsmall(S.rj, he) - (he == 2 ? 1 : 0), x1 = dsmall(S.rj + S.rw - 1, he) + (he == 2 ? 1 : 0);
     y0 = max(y0, 0);
     x0 = max(x0, 0);
     y1 = min(y1, S.ch[c] - 1);
@@ -1221,10 +1229,10 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
   for (int b = 0; b < S.bpm; b++) {
     int c = S.blk_comp[b], dx = S.blk_dx[b], dy = S.blk_dy[b], hs = S.hs[c], vs = S.vs[c];
     // bx = mx * hs + dx in [wx0, wx1]  <=>  mx in [mx_lo, mx_hi]
-    int mxl = S.wx0[c] - dx <= 0 ? 0 : (S.wx0[c] - dx + hs - 1) / hs;
-    int mxh = S.wx1[c] - dx < 0 ? -1 : (S.wx1[c] - dx) / hs;
-    int myl = S.wy0[c] - dy <= 0 ? 0 : (S.wy0[c] - dy + vs - 1) / vs;
-    int myh = S.wy1[c] - dy < 0 ? -1 : (S.wy1[c] - dy) / vs;
+    int mxl = S.wx0[c] - dx <= 0 ? 0 : dsmall(S.wx0[c] - dx + hs - 1, hs);
+    int mxh = S.wx1[c] - dx < 0 ? -1 : dsmall(S.wx1[c] - dx, hs);
+    int myl = S.wy0[c] - dy <= 0 ? 0 : dsmall(S.wy0[c] - dy + vs - 1, vs);
+    int myh = S.wy1[c] - dy < 0 ? -1 : dsmall(S.wy1[c] - dy, vs);
     // window-relative index of block (mx * hs + dx, my * vs + dy) is
     // base + my * (vs * wbw) + mx * hs (base may be negative: only window
     // blocks are ever addressed, and the sum wraps back in 32 bits)

@@ -17,9 +17,10 @@
 // Progressive, arithmetic, lossless, 12-bit, multi-scan and CMYK streams
 // return -1 (the device path reports FFCV_SAMPLE_UNSUPPORTED for them).
 // The tjTransform crop / mirror (enable_crop, hflip) is restated on the
-// coefficients (transform_coefs); TurboJPEG's scaled decoding is not: a
-// request that TurboJPEG would decode at a factor other than 1/1 returns -1.
-// ffcv itself passes the image's own size and False, False, 1, 1.
+// coefficients (transform_coefs); TurboJPEG's scaled decoding at 1/2, 1/4
+// and 1/8 too (decode_scaled, jidctred.c): a request TurboJPEG would decode
+// at another factor returns -1.  ffcv itself passes the image's own size and
+// False, False, 1, 1.
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -625,6 +626,242 @@ void upsample_row(const Dec &d, int ci, const uint8_t *pl, int stride, int y, in
   }
 }
 
+
+// jidctred.c (libjpeg-turbo): the reduced-size IDCTs tjDecompress2 runs at
+// scaling factors 1/2, 1/4, 1/8 (DCT_scaled_size 4, 2, 1 -- islow-style,
+// CONST_BITS 13, PASS1_BITS 2, the plain quantisation table as multipliers,
+// whatever dct_method says), with libjpeg's zero-AC shortcuts (value-neutral)
+constexpr int RCB = 13, RP1 = 2;
+constexpr int64_t F0_211164243 = 1730, F0_509795579 = 4176, F0_601344887 = 4926, F0_720959822 = 5906,
+                  F0_765366865 = 6270, F0_850430095 = 6967, F0_899976223 = 7373, F1_061594337 = 8697,
+                  F1_272758580 = 10426, F1_451774981 = 11893, F1_847759065 = 15137, F2_172734803 = 17799,
+                  F2_562915447 = 20995, F3_624509785 = 29692;
+inline int64_t rdesc(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
+
+void idct_4x4(const int16_t *in, const uint16_t *q, uint8_t *out, int stride, const uint8_t *rl) {
+  int64_t ws[32];
+  for (int c = 0; c < 8; c++) {
+    if (c == 4) continue;  // the second pass never reads column 4
+    const int16_t *ip = in + c;
+    const uint16_t *qp = q + c;
+    int64_t *w = ws + c;
+    if (!(ip[8] | ip[16] | ip[24] | ip[40] | ip[48] | ip[56])) {
+      const int64_t dc = (int64_t)(ip[0] * qp[0]) * (1 << RP1);
+      w[0] = w[8] = w[16] = w[24] = dc;
+      continue;
+    }
+    int64_t t0 = (int64_t)(ip[0] * qp[0]) * ((int64_t)1 << (RCB + 1));
+    const int64_t z2 = ip[16] * qp[16], z3 = ip[48] * qp[48];
+    const int64_t t2 = z2 * F1_847759065 - z3 * F0_765366865;
+    const int64_t t10 = t0 + t2, t12 = t0 - t2;
+    const int64_t y1 = ip[56] * qp[56], y2 = ip[40] * qp[40], y3 = ip[24] * qp[24], y4 = ip[8] * qp[8];
+    t0 = -y1 * F0_211164243 + y2 * F1_451774981 - y3 * F2_172734803 + y4 * F1_061594337;
+    const int64_t u2 = -y1 * F0_509795579 - y2 * F0_601344887 + y3 * F0_899976223 + y4 * F2_562915447;
+    w[0] = rdesc(t10 + u2, RCB - RP1 + 1);
+    w[24] = rdesc(t10 - u2, RCB - RP1 + 1);
+    w[8] = rdesc(t12 + t0, RCB - RP1 + 1);
+    w[16] = rdesc(t12 - t0, RCB - RP1 + 1);
+  }
+  for (int r = 0; r < 4; r++) {
+    const int64_t *w = ws + 8 * r;
+    uint8_t *o = out + (size_t)r * stride;
+    if (!(w[1] | w[2] | w[3] | w[5] | w[6] | w[7])) {
+      o[0] = o[1] = o[2] = o[3] = rl[rdesc(w[0], RP1 + 3) & 1023];
+      continue;
+    }
+    int64_t t0 = w[0] * ((int64_t)1 << (RCB + 1));
+    const int64_t t2 = w[2] * F1_847759065 - w[6] * F0_765366865;
+    const int64_t t10 = t0 + t2, t12 = t0 - t2;
+    const int64_t y1 = w[7], y2 = w[5], y3 = w[3], y4 = w[1];
+    t0 = -y1 * F0_211164243 + y2 * F1_451774981 - y3 * F2_172734803 + y4 * F1_061594337;
+    const int64_t u2 = -y1 * F0_509795579 - y2 * F0_601344887 + y3 * F0_899976223 + y4 * F2_562915447;
+    const int sh = RCB + RP1 + 3 + 1;
+    o[0] = rl[rdesc(t10 + u2, sh) & 1023];
+    o[3] = rl[rdesc(t10 - u2, sh) & 1023];
+    o[1] = rl[rdesc(t12 + t0, sh) & 1023];
+    o[2] = rl[rdesc(t12 - t0, sh) & 1023];
+  }
+}
+
+void idct_2x2(const int16_t *in, const uint16_t *q, uint8_t *out, int stride, const uint8_t *rl) {
+  int64_t ws[16];
+  for (int c = 0; c < 8; c++) {
+    if (c == 2 || c == 4 || c == 6) continue;  // not read by the second pass
+    const int16_t *ip = in + c;
+    const uint16_t *qp = q + c;
+    int64_t *w = ws + c;
+    if (!(ip[8] | ip[24] | ip[40] | ip[56])) {
+      const int64_t dc = (int64_t)(ip[0] * qp[0]) * (1 << RP1);
+      w[0] = w[8] = dc;
+      continue;
+    }
+    const int64_t t10 = (int64_t)(ip[0] * qp[0]) * ((int64_t)1 << (RCB + 2));
+    const int64_t t0 = -(int64_t)(ip[56] * qp[56]) * F0_720959822 + (int64_t)(ip[40] * qp[40]) * F0_850430095 -
+                       (int64_t)(ip[24] * qp[24]) * F1_272758580 + (int64_t)(ip[8] * qp[8]) * F3_624509785;
+    w[0] = rdesc(t10 + t0, RCB - RP1 + 2);
+    w[8] = rdesc(t10 - t0, RCB - RP1 + 2);
+  }
+  for (int r = 0; r < 2; r++) {
+    const int64_t *w = ws + 8 * r;
+    uint8_t *o = out + (size_t)r * stride;
+    if (!(w[1] | w[3] | w[5] | w[7])) {
+      o[0] = o[1] = rl[rdesc(w[0], RP1 + 3) & 1023];
+      continue;
+    }
+    const int64_t t10 = w[0] * ((int64_t)1 << (RCB + 2));
+    const int64_t t0 = -w[7] * F0_720959822 + w[5] * F0_850430095 - w[3] * F1_272758580 + w[1] * F3_624509785;
+    o[0] = rl[rdesc(t10 + t0, RCB + RP1 + 3 + 2) & 1023];
+    o[1] = rl[rdesc(t10 - t0, RCB + RP1 + 3 + 2) & 1023];
+  }
+}
+
+void idct_1x1(const int16_t *in, const uint16_t *q, uint8_t *out, int, const uint8_t *rl) {
+  out[0] = rl[rdesc((int64_t)(in[0] * q[0]), 3) & 1023];
+}
+
+// One upsampled component row at a scaled decode (jdsample.c's choice by the
+// component's sample group sizes): full size, h2v1 / h2v2 (fancy when fancy
+// and the row is wider than 2 samples, else replication), h1v2 fancy, or
+// integral replication.
+enum UpMode { UP_FULL, UP_H2V1, UP_H2V2, UP_H1V2, UP_INT };
+void upsample_row_mode(const uint8_t *pl, int stride, int cw, int ch, UpMode mode, bool fancy, int he, int ve, int y,
+                       int W, int *out) {
+  auto rowp = [&](int r) { return pl + (size_t)(r < 0 ? 0 : (r >= ch ? ch - 1 : r)) * stride; };
+  if (mode == UP_FULL) {
+    const uint8_t *r = pl + (size_t)y * stride;
+    for (int x = 0; x < W; x++) out[x] = r[x];
+  } else if (mode == UP_H2V1) {
+    const uint8_t *r = pl + (size_t)y * stride;
+    for (int x = 0; x < W; x++) {
+      const int col = x >> 1;
+      if (!fancy || cw <= 2)
+        out[x] = r[col];
+      else if (x & 1)
+        out[x] = col + 1 >= cw ? r[col] : (r[col] * 3 + r[col + 1] + 2) >> 2;
+      else
+        out[x] = col == 0 ? r[0] : (r[col] * 3 + r[col - 1] + 1) >> 2;
+    }
+  } else if (mode == UP_H1V2) {
+    const int row = y >> 1;
+    const uint8_t *a = rowp(row), *o = rowp(y & 1 ? row + 1 : row - 1);
+    const int bias = y & 1 ? 2 : 1;
+    for (int x = 0; x < W; x++) out[x] = (a[x] * 3 + o[x] + bias) >> 2;
+  } else if (mode == UP_H2V2) {
+    const int row = y >> 1;
+    if (!fancy || cw <= 2) {
+      for (int x = 0; x < W; x++) out[x] = pl[(size_t)row * stride + (x >> 1)];
+      return;
+    }
+    const uint8_t *a = rowp(row), *o = rowp(y & 1 ? row + 1 : row - 1);
+    thread_local std::vector<int> cs;
+    cs.resize((size_t)cw + 2);
+    int *c = cs.data() + 1;
+    for (int col = 0; col < cw; col++) c[col] = a[col] * 3 + o[col];
+    c[-1] = c[0];
+    c[cw] = c[cw - 1];
+    for (int x = 0; x + 1 < W; x += 2) {
+      const int col = x >> 1, t = c[col] * 3;
+      out[x] = (t + c[col - 1] + 8) >> 4;
+      out[x + 1] = (t + c[col + 1] + 7) >> 4;
+    }
+    if (W & 1) out[W - 1] = (c[(W - 1) >> 1] * 3 + c[((W - 1) >> 1) - 1] + 8) >> 4;
+  } else {
+    const uint8_t *r = pl + (size_t)(y / ve) * stride;
+    for (int x = 0; x < W; x++) out[x] = r[x / he];
+  }
+}
+
+// tjDecompress2 at 1/2, 1/4, 1/8 (sm = the luma DCT_scaled_size 4 / 2 / 1) of
+// the coefficients co[] (natural order, absolute DC, whole-MCU block grids):
+// libjpeg-turbo's jpeg_core_output_dimensions gives each component the
+// largest DCT size (doubling from sm, below 8) that its sampling still
+// divides, so 4:2:0 chroma decodes at twice the luma's size with no
+// upsampling; 8 is the ifast IDCT, 4 / 2 / 1 the reduced ones; fancy
+// upsampling is off at 1/8 (min DCT size 1).  Rows are packed at the
+// scaled width.
+const char *decode_scaled(const Dec &d, const std::vector<int16_t> co[3], int sm, uint8_t *out) {
+  const Tables &T = tables();
+  const int W = (d.W * sm + 7) / 8, H = (d.H * sm + 7) / 8;
+  const int mcux = (d.W + 8 * d.hmax - 1) / (8 * d.hmax), mcuy = (d.H + 8 * d.vmax - 1) / (8 * d.vmax);
+  thread_local std::vector<uint8_t> plane[3];
+  thread_local std::vector<int> rows[3];
+  int size[3], cw[3], ch[3], stride[3], he[3], ve[3];
+  UpMode mode[3];
+  const bool fancy = sm > 1;
+  for (int i = 0; i < d.nc; i++) {
+    const Comp &c = d.c[i];
+    int ss = sm;
+    while (ss < 8 && (d.hmax * sm) % (c.h * ss * 2) == 0 && (d.vmax * sm) % (c.v * ss * 2) == 0) ss *= 2;
+    size[i] = ss;
+    cw[i] = (int)(((int64_t)d.W * c.h * ss + (int64_t)d.hmax * 8 - 1) / ((int64_t)d.hmax * 8));
+    ch[i] = (int)(((int64_t)d.H * c.v * ss + (int64_t)d.vmax * 8 - 1) / ((int64_t)d.vmax * 8));
+    const int bw = mcux * c.h, bh = mcuy * c.v;
+    stride[i] = bw * ss;
+    plane[i].resize((size_t)stride[i] * bh * ss);
+    int16_t qf[64];
+    uint16_t qn[64];
+    for (int k = 0; k < 64; k++) {
+      qn[k] = d.qt[c.tq][k];
+      qf[k] = (int16_t)(((int64_t)d.qt[c.tq][k] * kAanScales[k] + (1 << 11)) >> 12);
+    }
+    for (int by = 0; by < bh; by++)
+      for (int bx = 0; bx < bw; bx++) {
+        const int16_t *b = co[i].data() + ((size_t)by * bw + bx) * 64;
+        uint8_t *o = plane[i].data() + (size_t)by * ss * stride[i] + (size_t)bx * ss;
+        if (ss == 8)
+          idct_ifast(b, qf, o, stride[i], T.rl);
+        else if (ss == 4)
+          idct_4x4(b, qn, o, stride[i], T.rl);
+        else if (ss == 2)
+          idct_2x2(b, qn, o, stride[i], T.rl);
+        else
+          idct_1x1(b, qn, o, stride[i], T.rl);
+      }
+    const int hin = c.h * ss / sm, vin = c.v * ss / sm;
+    he[i] = ve[i] = 1;
+    if (hin == d.hmax && vin == d.vmax)
+      mode[i] = UP_FULL;
+    else if (hin * 2 == d.hmax && vin == d.vmax)
+      mode[i] = UP_H2V1;
+    else if (hin * 2 == d.hmax && vin * 2 == d.vmax)
+      mode[i] = UP_H2V2;
+    else if (hin == d.hmax && vin * 2 == d.vmax && fancy)
+      mode[i] = UP_H1V2;
+    else {
+      if (d.hmax % hin || d.vmax % vin) return "fractional upsampling at this scale";
+      mode[i] = UP_INT;
+      he[i] = d.hmax / hin;
+      ve[i] = d.vmax / vin;
+    }
+    rows[i].resize((size_t)W);
+  }
+  for (int y = 0; y < H; y++) {
+    uint8_t *o = out + (size_t)y * W * 3;
+    if (d.nc == 1) {
+      const uint8_t *r = plane[0].data() + (size_t)y * stride[0];
+      for (int x = 0; x < W; x++) o[3 * x] = o[3 * x + 1] = o[3 * x + 2] = r[x];
+      continue;
+    }
+    for (int i = 0; i < 3; i++)
+      upsample_row_mode(plane[i].data(), stride[i], cw[i], ch[i], mode[i], fancy, he[i], ve[i], y, W, rows[i].data());
+    const int *r0 = rows[0].data(), *r1 = rows[1].data(), *r2 = rows[2].data();
+    for (int x = 0; x < W; x++) {
+      if (d.color_rgb) {
+        o[3 * x] = (uint8_t)r0[x];
+        o[3 * x + 1] = (uint8_t)r1[x];
+        o[3 * x + 2] = (uint8_t)r2[x];
+        continue;
+      }
+      const int yy = r0[x], cb = r1[x], cr = r2[x];
+      const int R = yy + T.cr_r[cr], G = yy + ((T.cb_g[cb] + T.cr_g[cr]) >> 16), B = yy + T.cb_b[cb];
+      o[3 * x] = (uint8_t)(R < 0 ? 0 : (R > 255 ? 255 : R));
+      o[3 * x + 1] = (uint8_t)(G < 0 ? 0 : (G > 255 ? 255 : G));
+      o[3 * x + 2] = (uint8_t)(B < 0 ? 0 : (B > 255 ? 255 : B));
+    }
+  }
+  return nullptr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -667,10 +904,28 @@ int imdecode(unsigned char *input_buffer, uint64_t input_size, uint32_t source_h
     ffcv::set_error("imdecode: the %dx%d image cannot be scaled into %ux%u", d.H, d.W, req_h, req_w);
     return -1;
   }
-  if (fn != fd) {
-    ffcv::set_error("imdecode: the %dx%d image would decode at scale %d/%d into %ux%u (scaled decoding is not "
-                    "supported)", d.H, d.W, fn, fd, req_h, req_w);
+  if (fn != fd && !(fn == 1 && (fd == 2 || fd == 4 || fd == 8))) {
+    ffcv::set_error("imdecode: the %dx%d image would decode at scale %d/%d into %ux%u (only 1/1, 1/2, 1/4 and "
+                    "1/8 are supported)", d.H, d.W, fn, fd, req_h, req_w);
     return -1;
+  }
+  if (fn != fd) {  // jidctred.c's reduced IDCTs (decode_scaled)
+    if (!transform) {  // the stream's coefficients
+      const int mcux = (d.W + 8 * d.hmax - 1) / (8 * d.hmax), mcuy = (d.H + 8 * d.vmax - 1) / (8 * d.vmax);
+      int bw[3];
+      for (int i = 0; i < d.nc; i++) {
+        bw[i] = mcux * d.c[i].h;
+        tco[i].assign((size_t)bw[i] * mcuy * d.c[i].v * 64, 0);
+      }
+      decode_scan(input_buffer, d, [&](int ci, int bx, int by, const int16_t *blk) {
+        std::memcpy(tco[ci].data() + ((size_t)by * bw[ci] + bx) * 64, blk, 64 * sizeof(int16_t));
+      });
+    }
+    if (const char *err = decode_scaled(d, tco, 8 / fd, output_buffer)) {
+      ffcv::set_error("imdecode: %s", err);
+      return -1;
+    }
+    return 0;
   }
   if (transform) {
     const Tables &T = tables();

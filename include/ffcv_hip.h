@@ -140,11 +140,12 @@ void resize(int64_t cresizer, int64_t source_p, int64_t sx, int64_t sy,
  * taken in the mirrored frame, the partial iMCU column at the right edge is
  * not mirrored).  As tjDecompress2 does, the decode runs at the largest
  * TurboJPEG scaling factor whose output fits the requested size (scaled by
- * scale_num / scale_denom), rows packed at the decoded width; only the
- * factor 1/1 is restated.  Returns 0, or -1 on a decode error, an
- * unsupported stream (progressive, arithmetic, multi-scan, CMYK), a
- * misaligned crop, or a request TurboJPEG would decode at another factor --
- * see ffcv_last_error().  ffcv itself passes the image's size, 0, 0, 1, 1,
+ * scale_num / scale_denom), rows packed at the decoded width; the factors
+ * 1/1, 1/2, 1/4 and 1/8 are restated (libjpeg's reduced IDCTs, bit-exact
+ * with libjpeg-turbo).  Returns 0, or -1 on a decode error, an unsupported
+ * stream (progressive, arithmetic, multi-scan, CMYK), a misaligned crop, or
+ * a request TurboJPEG would decode at another factor -- see
+ * ffcv_last_error().  ffcv itself passes the image's size, 0, 0, 1, 1,
  * False, False. */
 int imdecode(unsigned char *input_buffer, uint64_t input_size,
              uint32_t source_height, uint32_t source_width,

@@ -54,6 +54,8 @@ static size_t g_structsize;
 #define OFF_IMAGE_HEIGHT 52
 #define OFF_NUM_COMPONENTS 56
 #define OFF_OUT_COLOR_SPACE 64
+#define OFF_SCALE_NUM 68
+#define OFF_SCALE_DENOM 72
 #define OFF_DCT_METHOD 96
 #define OFF_DO_FANCY 100
 #define OFF_OUTPUT_WIDTH 136
@@ -117,8 +119,17 @@ size_t ljt_structsize(void) { return g_structsize; }
 /* Decode to interleaved RGB.  dct_method: 0 islow, 1 ifast.  fancy: 0/1.
  * Returns 0 on success; writes w/h/components.  out must hold w*h*3 bytes
  * (call with out=NULL to query geometry only). */
+int ljt_decode_scaled(const unsigned char *buf, unsigned long n, unsigned char *out,
+                      int dct_method, int fancy, int scale_num, int scale_denom, int *w, int *h, int *ncomp);
 int ljt_decode(const unsigned char *buf, unsigned long n, unsigned char *out,
                int dct_method, int fancy, int *w, int *h, int *ncomp) {
+  return ljt_decode_scaled(buf, n, out, dct_method, fancy, 1, 1, w, h, ncomp);
+}
+
+/* As ljt_decode, with libjpeg's DCT scaling (scale_num / scale_denom: the
+ * output size TurboJPEG's tjDecompress2 asks for at a scaling factor). */
+int ljt_decode_scaled(const unsigned char *buf, unsigned long n, unsigned char *out,
+                      int dct_method, int fancy, int scale_num, int scale_denom, int *w, int *h, int *ncomp) {
   if (!g_structsize) return -10;
   unsigned char *cinfo = (unsigned char *)calloc(1, 4096);
   err_wrap *ew = (err_wrap *)calloc(1, sizeof(err_wrap));
@@ -138,6 +149,8 @@ int ljt_decode(const unsigned char *buf, unsigned long n, unsigned char *out,
   *(int *)(cinfo + OFF_OUT_COLOR_SPACE) = JCS_RGB;
   *(int *)(cinfo + OFF_DCT_METHOD) = dct_method;
   *(int *)(cinfo + OFF_DO_FANCY) = fancy;
+  *(unsigned *)(cinfo + OFF_SCALE_NUM) = (unsigned)scale_num;
+  *(unsigned *)(cinfo + OFF_SCALE_DENOM) = (unsigned)scale_denom;
   *ncomp = *(int *)(cinfo + OFF_NUM_COMPONENTS);
   p_start(cinfo);
   *w = (int)*(unsigned *)(cinfo + OFF_OUTPUT_WIDTH);

@@ -237,6 +237,9 @@ def ljt():
         l.ljt_decode.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p]
+        l.ljt_decode_scaled.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         if l.ljt_open(path.encode()) != 0:
             return None
         _ljt = l
@@ -252,20 +255,21 @@ def use_libjpeg_turbo(enable=True):
     return l is not None
 
 
-def ljt_decode(data, dct='ifast', fancy=True):
-    """tjDecompress2(TJPF_RGB, TJFLAG_FASTDCT) semantics via libjpeg-turbo itself."""
+def ljt_decode(data, dct='ifast', fancy=True, scale=(1, 1)):
+    """tjDecompress2(TJPF_RGB, TJFLAG_FASTDCT) semantics via libjpeg-turbo itself
+    (scale: libjpeg's scale_num / scale_denom, TurboJPEG's scaling factor)."""
     l = ljt()
     data = bytes(data)
     w, h, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     buf = ctypes.create_string_buffer(data, len(data))
-    rc = l.ljt_decode(buf, len(data), None, 1 if dct == 'ifast' else 0, int(fancy),
-                      ctypes.byref(w), ctypes.byref(h), ctypes.byref(nc))
+    m = 1 if dct == 'ifast' else 0
+    rc = l.ljt_decode_scaled(buf, len(data), None, m, int(fancy), int(scale[0]), int(scale[1]),
+                             ctypes.byref(w), ctypes.byref(h), ctypes.byref(nc))
     if rc:
         raise ValueError(f'libjpeg error {rc}')
     out = np.zeros((h.value, w.value, 3), np.uint8)
-    rc = l.ljt_decode(buf, len(data), ctypes.c_void_p(out.ctypes.data),
-                      1 if dct == 'ifast' else 0, int(fancy), ctypes.byref(w),
-                      ctypes.byref(h), ctypes.byref(nc))
+    rc = l.ljt_decode_scaled(buf, len(data), ctypes.c_void_p(out.ctypes.data), m, int(fancy),
+                             int(scale[0]), int(scale[1]), ctypes.byref(w), ctypes.byref(h), ctypes.byref(nc))
     if rc:
         raise ValueError(f'libjpeg error {rc}')
     return out

@@ -86,7 +86,9 @@ def test_cpu_imdecode_rejects(hip_lib):
     # ... 45 x 63 fits 9/8, a scaled decode this restatement does not do
     assert L.imdecode(blob, np.zeros((45, 63, 3), np.uint8), 40, 56, 45, 63) == -1
     assert b'scale 9/8' in L.lib().ffcv_last_error()
-    assert L.imdecode(blob, out, 40, 56, 40, 56, 0, 0, 1, 2) == -1  # 1/2: reduced IDCT, not restated
+    # 3/8 (jidctint.c's 3x3 IDCT) is not restated; 1/2, 1/4, 1/8 are (below)
+    assert L.imdecode(blob, np.zeros((15, 21, 3), np.uint8), 40, 56, 40, 56, 0, 0, 3, 8) == -1
+    assert b'scale 3/8' in L.lib().ffcv_last_error()
     # the lossless crop's origin must be on an iMCU boundary (16 x 16 at 4:2:0)
     assert L.imdecode(blob, out, 40, 56, 24, 24, 8, 0, enable_crop=True) == -1
     assert b'iMCU' in L.lib().ffcv_last_error()
@@ -161,6 +163,40 @@ def test_cpu_imdecode_transform(hip_lib):
     assert np.array_equal(dec(bg, 40, 67, 16, 16, 8, 8, crop=True, flip=True), fl[8:24, 8:24])
     # hflip alone still crops with the given offsets and size (libffcv.cpp:89-93)
     assert np.array_equal(dec(bg, 40, 67, 16, 24, 16, 8, flip=True), fl[8:24, 16:40])
+
+
+def test_cpu_imdecode_scaled_matches_libjpeg_turbo(hip_lib, oracle):
+    """libffcv.cpp:101-103 tjDecompress2 at scaling factors 1/2, 1/4, 1/8
+    (scale_num / scale_denom): jidctred.c's reduced IDCTs, libjpeg-turbo's
+    per-component DCT sizes (4:2:0 chroma at twice the luma's size, no
+    upsampling), non-fancy upsampling at 1/8 -- bit-exact against
+    libjpeg-turbo 3.1.4 itself (the harness sets scale_num / scale_denom)."""
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(5)
+    cases = []
+    for h, w in [(61, 83), (64, 64), (17, 33), (120, 91), (9, 7)]:
+        img = natural_image(rng, h, w)
+        cases += [(img, encode_jpeg(img, 90, '4:2:0')), (img, encode_jpeg(img, 85, '4:2:2')),
+                  (img, encode_jpeg(img, 95, '4:4:4')), (img[:, :, 0].copy(), _pil(img[:, :, 0].copy(), quality=90)),
+                  (img, _pil(img, quality=90, subsampling=2))]
+    bad = []
+    for img, b in cases:
+        h, w = img.shape[:2]
+        for den in (2, 4, 8):
+            want = oracle.ljt_decode(b, scale=(1, den))
+            out = np.zeros(want.shape, np.uint8)
+            rc = L.imdecode(b, out, h, w, h, w, 0, 0, 1, den, False, False)
+            if rc != 0 or not np.array_equal(out, want):
+                bad.append((h, w, den, rc))
+    assert not bad, bad
+    # crop then scale: at 4:4:4 (no upsampling) each block scales on its own,
+    # so a block-aligned crop at 1/2 is the crop of the 1/2 decode
+    img = natural_image(rng, 72, 100)
+    b = _pil(img, quality=90, subsampling=0)
+    half = oracle.ljt_decode(b, scale=(1, 2))
+    out = np.zeros((12, 20, 3), np.uint8)
+    assert L.imdecode(b, out, 72, 100, 24, 40, 16, 8, 1, 2, True, False) == 0
+    assert np.array_equal(out, half[4:16, 8:28])
 
 
 def test_cpu_decode_batch(hip_lib, oracle):

@@ -1686,8 +1686,30 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const bool have = k < a.batch;
   ffcv_sample smp = {};
   int rng_err = 0;
+  // The workgroup's draws (draw_kernel fused): all in wave 0, lane 3 w + part
+  // for image w, so the MT19937 seeding chain runs once per workgroup instead
+  // of once per wave; the crops are read by every wave's parse after the
+  // barrier that follows the header staging (a workgroup fence: same CU)
+  __shared__ int s_rngerr[JW * IPW];
+  if (a.table && a.do_draw) {
+    if (threadIdx.x < JT) {
+      int err = 0;
+      if (threadIdx.x < 3 * JW * IPW) {
+        const int w = threadIdx.x / 3, part = threadIdx.x % 3;
+        const int sw = blockIdx.x * (JW * IPW) + w;
+        const int kw = a.k1_order && sw < a.batch ? (int)a.k1_order[sw] : sw;
+        if (kw < a.batch) {
+          const uint64_t idw = a.ids[kw];
+          const uint32_t hw = idw < a.n_table ? a.table[idw].height : 1u, ww = idw < a.n_table ? a.table[idw].width : 1u;
+          err = draw_part(part, kw, idw, hw, ww, a.dp, a.crops_w, a.cut_w, a.flips_w);
+        }
+      }
+      const uint64_t eb = __ballot(err != 0);
+      if (threadIdx.x < JW * IPW) s_rngerr[threadIdx.x] = ((eb >> (3 * threadIdx.x)) & 7ull) != 0;
+    }
+  }
   if (have) {
-    if (a.table) {  // fused gather (gather_samples_kernel) + draws (draw_kernel)
+    if (a.table) {  // fused gather (gather_samples_kernel)
       const uint64_t id = a.ids[k];
       if (id < a.n_table) {
         smp = a.table[id];
@@ -1695,10 +1717,6 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
         smp.height = smp.width = 1;
       }
       if (t == 0 && a.samples_out) a.samples_out[k] = smp;
-      if (a.do_draw && t >= 1 && t <= 3)
-        rng_err = draw_part(t - 1, k, id, smp.height, smp.width, a.dp, a.crops_w, a.cut_w, a.flips_w);
-      rng_err = seg_any(rng_err != 0, sg);
-      wsync_mem();  // the crop (lane 1) is read by parse_header (lane 0)
     } else {
       smp = a.samples[k];
     }
@@ -1743,7 +1761,12 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       }
     }
   }
-  wsync_lds();
+  if (a.table && a.do_draw) {  // the draws (wave 0) are done; waves 1.. staged their headers meanwhile
+    __syncthreads();
+    rng_err = s_rngerr[wi];
+  } else {
+    wsync_lds();
+  }
   STAMP(10);
 #if defined(K1_STOP) && K1_STOP == 7  // timing only: gather, draws and header staging
   if (smp.size != 0x7fffffffffffull) return;

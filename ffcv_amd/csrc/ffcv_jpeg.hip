@@ -683,9 +683,9 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
 #ifndef K1_TIMING_NOAC
     {  // a staged block that ends leaves as three 16-byte stores
       const bool fl = bend && stg && inwin;
+      // left undefined where the lane does not flush (its stores go out of
+      // range): zeroing it cost 12 moves per step
       uint4 c[ACS_BYTES / 16];
-#pragma unroll
-      for (int q = 0; q < ACS_BYTES / 16; q++) c[q] = make_uint4(0, 0, 0, 0);
       if (fl) {
 #pragma unroll
         for (int q = 0; q < ACS_BYTES / 16; q++) {

@@ -498,11 +498,40 @@ def test_bench_rccl_world1():
            '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.join(root, 'bench.py'),
            '--gpus', '1', '--steps', '6', '--warmup', '2', '--unique', '512', '--dataset-size', '40000',
            '--no-cpu-baseline', '--no-later-epochs', '--no-c5', '--parity-rows', '256']
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=root)
+    # the environment as the driver's run gets it (the box exports
+    # HSA_ENABLE_IPC_MODE_LEGACY=0 itself; bench.py's self-launch keeps it)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
     pg = line['process_group']
     assert pg['backend'] == 'nccl' and pg['world_size'] == 1, pg
     assert line['n_gpus'] == 1 and line['value'] > 0
     assert line['parity']['checked'] > 0 and line['parity']['mismatch'] == 0
+
+
+def test_bench_gpus2_self_launch():
+    """`bench.py --gpus 2` with no torchrun around it
+    starts torchrun itself (a child process) with two ranks, each re-entering
+    bench.py with RANK / WORLD_SIZE set; on this one-GPU box both ranks share
+    cuda:0 over a gloo group (RCCL refuses two ranks on one device).  The line
+    must report n_gpus 2, a world-2 process group with both ranks' timings,
+    and green parity on every rank."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '6', '--warmup', '2',
+           '--unique', '512', '--dataset-size', '40000', '--no-cpu-baseline', '--no-later-epochs', '--no-c5',
+           '--parity-rows', '256']
+    env = dict(os.environ, FFCV_BENCH_BACKEND='gloo')
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert 'torch.distributed.run' in r.stderr
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
+    pg = line['process_group']
+    assert pg['backend'] == 'gloo' and pg['world_size'] == 2, pg
+    assert [p['rank'] for p in pg['per_rank']] == [0, 1]
+    assert line['n_gpus'] == 2 and line['config']['global_batch'] == 2 * 512
+    assert abs(line['value'] - 2 * 512 * 6 / max(p['seconds'] for p in pg['per_rank'])) < 0.01 * line['value']
+    par = line['parity']
+    assert par['checked_all_ranks'] > par['checked'] > 0 and par['mismatch_all_ranks'] == 0

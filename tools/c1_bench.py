@@ -53,11 +53,15 @@ def main():
         for images, labels in loader:
             n += images.shape[0]
         times.append(time.perf_counter() - t0)
-    # exactness of the last batch against the source
-    first = next(iter(loader))[0].numpy()
-    assert np.array_equal(first, imgs[:512])
+    # exactness of the first batch (images and labels) against the source
+    first, first_labels = next(iter(loader))
+    ok = bool(np.array_equal(first.numpy(), imgs[:512])
+              and np.array_equal(np.asarray(first_labels).reshape(-1), np.arange(512) % 10))
+    assert ok, 'C1 first batch differs from the source samples'
     best = min(times[1:])
     print(json.dumps({'config': 'C1: raw 32x32 + int, batch 512, SEQUENTIAL, drop_last, CPU Loader',
+                      'value': round(n / best, 1), 'unit': 'images/s',
+                      'first_batch_exact': ok,
                       'samples_per_epoch': n, 'epoch_s_best': round(best, 5),
                       'images_per_s': round(n / best, 1), 'epoch_s_all': [round(t, 5) for t in times],
                       'first_epoch_s': round(times[0], 5), 'write_s': round(t_write, 2),

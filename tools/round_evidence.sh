@@ -14,7 +14,7 @@ timeout -k 10 300 python bench.py --config c5 --steps 200 --warmup 20 --unique 1
 timeout -k 10 300 python bench.py --config c2 --steps 200 --warmup 20 --unique 10000 > gpurun_out/${TAG}_bench_c2.log 2>&1
 timeout -k 10 300 python bench.py --entropy-index --no-cpu-baseline --no-c5 > gpurun_out/${TAG}_bench_eidx.log 2>&1
 # N > 1 rehearsal on one GPU: two ranks, gloo barrier (the driver's 8-GPU run uses RCCL)
-FFCV_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 40 --warmup 10 --no-cpu-baseline --no-later-epochs > gpurun_out/${TAG}_bench_2rank.log 2>&1
+FFCV_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 40 --warmup 10 --no-cpu-baseline --no-later-epochs > gpurun_out/${TAG}_bench_2rank.log 2>&1
 for f in bench_driver bench bench_c5 bench_c2 bench_eidx bench_2rank; do tail -1 gpurun_out/${TAG}_$f.log | cut -c1-200; done
 # every profiled launch the same size (C3 / C2: 24 batches per launch, warmup = one launch)
 bash tools/profile.sh ${TAG}_c3 --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches

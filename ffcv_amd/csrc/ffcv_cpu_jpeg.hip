@@ -533,8 +533,14 @@ const char *transform_coefs(const uint8_t *b, Dec &d, uint32_t x, uint32_t y, ui
   const int imw = 8 * d.hmax, imh = 8 * d.vmax;
   if (x % (uint32_t)imw || y % (uint32_t)imh) return "crop origin is not on an iMCU boundary";
   if (x >= (uint32_t)d.W || y >= (uint32_t)d.H) return "crop origin outside the image";
-  const int rw = (int)(w == 0 || w > (uint32_t)d.W - x ? (uint32_t)d.W - x : w);
-  const int rh = (int)(h == 0 || h > (uint32_t)d.H - y ? (uint32_t)d.H - y : h);
+  // jtransform_request_workspace: a set crop size must fit from its origin
+  // (JERR_BAD_CROP_SPEC); crop extension (w > W) is refused here whether or
+  // not a transform is requested (libjpeg-turbo allows it only without one,
+  // padding the image: not restated)
+  if (w != 0 && (w > (uint32_t)d.W || x > (uint32_t)d.W - w)) return "bad crop spec (width)";
+  if (h != 0 && (h > (uint32_t)d.H || y > (uint32_t)d.H - h)) return "bad crop spec (height)";
+  const int rw = (int)(w == 0 ? (uint32_t)d.W - x : w);
+  const int rh = (int)(h == 0 ? (uint32_t)d.H - y : h);
   // source coefficients, whole-MCU grids (blocks a non-interleaved scan does not code stay zero)
   const int mcux = (d.W + imw - 1) / imw, mcuy = (d.H + imh - 1) / imh;
   std::vector<int16_t> src[3];

@@ -143,9 +143,16 @@ def test_cpu_imdecode_transform(hip_lib):
     b444 = _pil(img, quality=90, subsampling=0)
     f444 = dec(b444, 72, 100, 72, 100)
     assert np.array_equal(dec(b444, 72, 100, 24, 40, 16, 8, crop=True), f444[8:32, 16:56])
-    # clamped to the image (TJ: r.w past the edge -> to the edge), rows packed at the clamped width
-    c = dec(b444, 72, 100, 20, 56, 48, 56, crop=True)  # real 16 x 52 (9/8 would need 18 x 59)
-    assert np.array_equal(c.reshape(-1)[:16 * 52 * 3].reshape(16, 52, 3), f444[56:, 48:])
+    # a set crop size past the image edge is refused, as transupp.c's
+    # jtransform_request_workspace does (JERR_BAD_CROP_SPEC: tjTransform and
+    # so the reference's imdecode return -1); size 0 still means "to the edge"
+    out = np.zeros((20, 56, 3), np.uint8)
+    assert L.imdecode(b444, out, 72, 100, 20, 56, 48, 56, 1, 1, True, False) == -1
+    assert b'bad crop spec' in L.lib().ffcv_last_error()
+    assert L.imdecode(b444, out, 72, 100, 16, 56, 48, 56, 1, 1, True, False) == -1  # x + w > W
+    assert L.imdecode(b444, out, 72, 100, 20, 52, 48, 56, 1, 1, True, False) == -1  # y + h > H
+    edge = dec(b444, 72, 100, 16, 52, 48, 56, crop=True)  # exactly to the corner
+    assert np.array_equal(edge, f444[56:, 48:])
     # 4:2:0: away from the crop's borders the fancy upsampling sees the same chroma
     c = dec(b420, 72, 100, 40, 48, 32, 16, crop=True)
     assert np.array_equal(c[2:-2, 2:-2], full[18:54, 34:78])

@@ -396,7 +396,6 @@ def main():
     ap.add_argument('--no-host-check', action='store_true',
                     help='profiling runs: do not fail when submission dominates (the profiler slows the host)')
     ap.add_argument('--lib', default=None, help='diagnostic A/B: load this build of libffcv_hip.so')
-    ap.add_argument('--k2flags', type=int, default=0, help='diagnostic: K2 timing-only flags')
     ap.add_argument('--only', type=int, default=0,
                     help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 1 IDCT, bit 2 K2)')
     ap.add_argument('--split', default='',
@@ -641,8 +640,8 @@ def main():
     for sl in slots:
         sl['status'].fill_(-1)
         sl['used'] = 0
-        if (args.only or args.k2flags) and sl['dec'] is not None:  # diagnostic kernel selection
-            sl['dec'].set_diag(only=args.only or 7, k2flags=args.k2flags)
+        if args.only and sl['dec'] is not None:  # diagnostic kernel selection
+            sl['dec'].set_diag(only=args.only)
     # per-kernel HIP events inside the library (ffcv_jpeg_set_timing): each
     # timed launch records events on its own stream around K1, K1b and K2
     kernel_events = mode == 'jpg' and not args.no_kernel_events
@@ -687,7 +686,7 @@ def main():
         per_rank = [float(x.item()) for x in allt]
         elapsed = max(per_rank)
     parity = None
-    if args.parity_rows > 0 and not (args.only or args.k2flags):
+    if args.parity_rows > 0 and not args.only:
         parity = parity_check(args.config, slots, order, batch, tile, offs, sizes, hs, ws, args.parity_rows)
         if dist:
             t = torch.tensor([parity['checked'], parity['mismatch'], parity['crop_mismatch']], dtype=torch.int64,
@@ -745,7 +744,7 @@ def main():
     # filling the index), then the same K steps are timed as epoch 1 (new crops,
     # no sync rounds).  Output is bit-identical with or without the index.
     later = None
-    if mode == 'jpg' and eidx is None and not args.no_later_epochs and not (args.only or args.k2flags):
+    if mode == 'jpg' and eidx is None and not args.no_later_epochs and not args.only:
         lidx = torch.zeros((N, L.EIDX_LANES, L.EIDX_WORDS), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()  # zeroed (default stream) before the slot streams publish into it
         for sl in slots:
@@ -812,14 +811,14 @@ def main():
     # as the rocprofv3 passes' uniform launches) ran
     k2e = os.environ.get('FFCV_K2_LOOP')
     k2_min = 8192 if k2e is None else (0 if k2e.strip() not in ('0', '') else 1 << 62)
-    k2_loop = cap >= k2_min and not args.k2flags
+    k2_loop = cap >= k2_min
     k2 = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>' if k2_loop else
           f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
     kernels = ['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', k2] if mode == 'jpg' else ['rrc_raw_kernel<false>']
     # the timed launches' own K2 (the driver's 20 steps: launches of 2,048-4,096
     # images, the per-band kernel) for the whole-path figures (path, traffic)
     k2t = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>'
-           if max(launch_imgs) >= k2_min and not args.k2flags else
+           if max(launch_imgs) >= k2_min else
            f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
     timed_kernels = kernels[:2] + [k2t] if mode == 'jpg' else kernels
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
@@ -1023,7 +1022,7 @@ def main():
         res['later_epochs'] = later
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(args.config, tile, offs, sizes, hs, ws, args.cpu_budget)
-    if rank == 0 and world == 1 and args.config == 'c3' and not args.no_c5 and not (args.only or args.k2flags):
+    if rank == 0 and world == 1 and args.config == 'c3' and not args.no_c5 and not args.only:
         res['c5'] = sub_result('c5')
         res['c2'] = sub_result('c2')
         res['c1'] = c1_result()

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, 'libffcv_hip.so')
 SOURCES = ['ffcv_common.hip', 'ffcv_rrc.hip', 'ffcv_jpeg.hip', 'ffcv_host.hip', 'ffcv_cpu_jpeg.hip']
-HEADERS = ['api_internal.h', 'device_common.h']
+HEADERS = ['api_internal.h', 'device_common.h', 'diag_hooks.h']
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950').split(';')[0]
 
 FLAGS = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-shared', '-std=c++17',

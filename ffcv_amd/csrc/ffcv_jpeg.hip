@@ -54,6 +54,7 @@
 
 #include "api_internal.h"
 #include "device_common.h"
+#include "diag_hooks.h"
 
 #define JT 64           // lanes per wave
 // JL = 32 (two images per wave, each with twice the bits per lane) is
@@ -313,13 +314,6 @@ struct BitReader {
 };
 
 
-// Loop-iteration counters for tools/jpeg_phases.py: a build with
-// -DFFCV_K1_DIAG only (they cost two instructions per decode step).
-#ifdef FFCV_K1_DIAG
-#define K1_DIAG(x) x
-#else
-#define K1_DIAG(x)
-#endif
 
 struct DecState {
   uint32_t pos;
@@ -647,7 +641,6 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     pos += nbits;
     // three stores every step (see BufReader): DC difference, first and
     // second AC coefficient, each out of range when the lane has none
-#ifndef K1_TIMING_NOSTORE
     const uint32_t o1 = (boff + (uint32_t)min(z + zinc - 1, 63)) * 2, o2 = (boff + (uint32_t)min(z + zadd - 1, 63)) * 2;
     {  // DC: the difference itself (coefficient output) or this lane's running sum
       const int rsum = (cc == 0 ? r0 : (cc == 1 ? r1 : r2)) + v;
@@ -659,28 +652,17 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
       else if (isblk && inwin)
         acs16[0] = (int16_t)rsum;  // a DC step starts the block: this lane stages it
     }
-#ifndef K1_TIMING_NOAC
     const int p1 = min(z + zinc - 1, 63), p2 = min(z + zadd - 1, 63);
     const bool a1 = z != 0 && size && inwin && alive, a2 = size2 && inwin && alive;
     const bool l1 = a1 && stg && p1 < ACS_Z, l2 = a2 && stg && p2 < ACS_Z;
     if (l1) acs16[p1] = (int16_t)v;
     if (l2) acs16[p2] = (int16_t)v2;
-#ifdef K1_STORE_MASKED
-    if (a1 && !l1) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, o1, 0, 0);
-    if (a2 && !l2) __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, o2, 0, 0);
-#elif defined(K1_TIMING_NODIRECT)
-    if (o1 == 0x12345u && o2 == 0x12345u) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, o1, 0, 0);
-#else
+    // (issuing these under exec masks instead measured 0.6-2% slower: K1's
+    // refill would then wait for every pending store, see BufReader)
     __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, a1 && !l1 ? o1 : BUF_OOR, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, a2 && !l2 ? o2 : BUF_OOR, 0, 0);
-#endif
-#endif
-#else  // timing only (wrong output): the write pass without its stores
-    if (v == 0x7fffffff && v2 == 0x7fffffff) __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, boff, 0, 0);
-#endif
     z += zadd;
     const bool bend = z >= 64;
-#ifndef K1_TIMING_NOAC
     {  // a staged block that ends leaves as three 16-byte stores
       const bool fl = bend && stg && inwin;
       // left undefined where the lane does not flush (its stores go out of
@@ -694,18 +676,11 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
         }
       }
       const uint32_t fo = fl ? boff * 2 : BUF_OOR;
-#ifdef K1_FLUSH_MASKED
-      if (fl)
-#endif
-#ifdef K1_TIMING_NOFLUSH
-      if (fo == 0x12345u)
-#endif
 #pragma unroll
       for (int q = 0; q < ACS_BYTES / 16; q++)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, c[q]), crs, fo + 16 * q, 0, 0);
     }
     stg = stg || bend;
-#endif
     // the next block: (blk + 1, nph, mx', my')
     const bool wrap = nph == 0;
     const int nmx = wrap ? (mx + 1 == mcux ? 0 : mx + 1) : mx;
@@ -728,14 +703,12 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
   rs0 = r0;
   rs1 = r1;
   rs2 = r2;
-#ifndef K1_TIMING_NOAC
   if (stg && z > 0 && inwin) {  // stopped inside a staged block: its positions below z are this lane's
     for (int q = 0; q < ACS_Z; q++) {
       const int c = acs16[q];
       if (q < z && c != 0) __builtin_amdgcn_raw_buffer_store_b16((short)c, crs, (boff + (uint32_t)q) * 2, 0, 0);
     }
   }
-#endif
 }
 
 // Cross-lane helpers on DPP (no LDS round trip, unlike __shfl's
@@ -942,11 +915,6 @@ struct JpegArgs {
   uint32_t max_h, max_w;
   uint64_t max_blocks;
   uint64_t *dbg;
-  int k2flags;  // diagnostics: bit 0 disables the K2 plane tiles, bit 1 the tap tables, bit 2 pixel pairs;
-                // timing only (wrong output): bit 3 skips the colour pass, bit 4 the resize arithmetic;
-                // bit 5 disables the separable linear resize, bit 6 the 4:2:0 quad colour pass,
-                // bit 7 the linear fast path; timing only: bits 8 / 9 / 10 skip the fast
-                // path's colour pass / column walk / tile staging
   int diag_only;  // host side only: kernels the launch runs (ffcv_jpeg_set_diag)
   // Entropy index (ffcv_jpeg_set_entropy_index): per dataset sample, the
   // converged start state of every lane range of the sync pass.  A sample
@@ -1508,9 +1476,7 @@ FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, 
 
   // ------------------------------------------------------------- P5 ----
   STAMP(5);
-#if defined(K1_STOP) && K1_STOP == 4  // timing only: K1 up to the sync pass (no write pass)
-  if (nthr != 0x7fffffffu) return any_bad;
-#endif
+  K1_STOP_AT(4, nthr != 0x7fffffffu, any_bad);  // diagnostics: K1 up to the sync pass (no write pass)
   zero_window_coefs(S, coef, t);
   uint32_t it_lane2 = 0;
   start_blk = blk_base;
@@ -1727,6 +1693,10 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     a.status[k] = FFCV_SAMPLE_OK;
     info->status = -1;  // K2 skips
   }
+  // no reservation until alloc_scratch makes one: an image that fails before
+  // it (draws, parse, raw) must not report the previous launch's region
+  // (ffcv_jpeg_arena_regions)
+  if (have && t == 0) info->arena_need = 0;
   const uint8_t *src = wave_uniform(a.base + smp.offset);
   const uint32_t nbytes = wuni((uint32_t)smp.size);  // uniform: sizes buffer resources
   auto fail = [&]() {
@@ -1768,9 +1738,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     wsync_lds();
   }
   STAMP(10);
-#if defined(K1_STOP) && K1_STOP == 7  // timing only: gather, draws and header staging
-  if (smp.size != 0x7fffffffffffull) return;
-#endif
+  K1_STOP_AT(7, smp.size != 0x7fffffffffffull);  // diagnostics: gather, draws and header staging
   if (t == 0) S.src = src;
   if (JL == JT || t == 0) {  // the whole wave runs the (scalar) parse; see parse_header
     int st = live ? (rng_err ? FFCV_SAMPLE_RNG : parse_header(S, wave_uniform(src), nbytes, smp, a, k, MODE)) : -1;
@@ -1779,9 +1747,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   }
   __syncthreads();
 
-#if defined(K1_STOP) && K1_STOP == 8  // timing only: up to the parse and the scratch allocation
-  if (smp.size != 0x7fffffffffffull) return;
-#endif
+  K1_STOP_AT(8, smp.size != 0x7fffffffffffull);  // diagnostics: up to the parse and the scratch allocation
   // ------------------------------------------------------------- P1 ----
   // The workgroup's first valid image provides the shared tables; every
   // image whose table slots and DHT bytes equal that image's uses them.
@@ -1857,9 +1823,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const uint64_t cf_off = ((uint64_t)wuni((uint32_t)(S.cf_off >> 32)) << 32) | wuni((uint32_t)S.cf_off);
   int16_t *coef = (int16_t *)(a.arena + cf_off);
 
-#if defined(K1_STOP) && K1_STOP == 1  // timing only: K1 up to the tables (no de-stuff)
-  if (cf_off != 0x7fffffffffffull) return;
-#endif
+  K1_STOP_AT(1, cf_off != 0x7fffffffffffull);  // diagnostics: K1 up to the tables (no de-stuff)
   // ------------------------------------------------------------- P2 ----
   // De-stuffing in stream order: each step the wave reads 64 consecutive
   // aligned dwords of the segment (one per lane), keeps every byte except a
@@ -1993,9 +1957,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     flush((dlen + STREAM_PAD + 3) & ~3u);
   }
   wsync_mem();
-#if defined(K1_STOP) && K1_STOP == 2  // timing only: K1 up to the de-stuffed stream
-  if (dlen != 0x7fffffffu) return;
-#endif
+  K1_STOP_AT(2, dlen != 0x7fffffffu);  // diagnostics: K1 up to the de-stuffed stream
   // one image per wave: its stream base is wave-uniform (scalar registers,
   // so the refill loads use the scalar-base + 32-bit offset form)
   const uint32_t *words = wave_uniform((const uint32_t *)gds);
@@ -2007,9 +1969,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF)
                              : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF);
   wsync_mem();
-#if defined(K1_STOP) && K1_STOP == 5  // timing only: K1 up to the write pass
-  if (!any_bad) return;
-#endif
+  K1_STOP_AT(5, !any_bad);  // diagnostics: K1 up to the write pass
 
   // ------------------------------------------------------------- P6 ----
   // DC prediction (jdhuff.c last_dc_val) for the coefficient output (JM_COEF;
@@ -2086,9 +2046,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
   }
   wsync_mem();
-#if defined(K1_STOP) && K1_STOP == 6  // timing only: K1 up to the DC prediction
-  if (!any_bad) return;
-#endif
+  K1_STOP_AT(6, !any_bad);  // diagnostics: K1 up to the DC prediction
 
   if (MODE == JM_COEF) {
     int16_t *o = (int16_t *)a.out + a.out_stride / 2 * k;
@@ -2529,7 +2487,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   auto p2 = [](int x) { return x == 1 || x == 2 || x == 4; };
   const bool pow2 = p2(G.he[0]) && p2(G.ve[0]) && p2(G.he[1]) && p2(G.ve[1]) && p2(G.he[2]) && p2(G.ve[2]);
   if (!GENERAL_ONLY && P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && pow2 &&
-      !(a.k2flags & 128)) {
+      true) {
     const int lut_b = FP16 ? 1536 : 0;
     LinTap *rtab = (LinTap *)(lds + lut_b);
     int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
@@ -2569,7 +2527,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       uint32_t sv[3][SU];
 #pragma unroll
       for (int c = 0; c < 3; c++) {
-        const int wpr = max(tpitch[c] >> 2, 1), n = (a.k2flags & 1024) ? 0 : trows[c] * (tpitch[c] >> 2);
+        const int wpr = max(tpitch[c] >> 2, 1), n = trows[c] * (tpitch[c] >> 2);
         const float rwp = __builtin_amdgcn_rcpf((float)wpr);  // (1 ulp: far inside the +0.5 margin)
         const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
 #pragma unroll
@@ -2582,7 +2540,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         uint32_t *tl = (uint32_t *)(lds + toff[c]);
-        const int wpr = max(tpitch[c] >> 2, 1), n = (a.k2flags & 1024) ? 0 : trows[c] * (tpitch[c] >> 2);
+        const int wpr = max(tpitch[c] >> 2, 1), n = trows[c] * (tpitch[c] >> 2);
 #pragma unroll
         for (int u = 0; u < SU; u++)
           if (u * K2T + t < n) tl[u * K2T + t] = sv[c][u];
@@ -2596,8 +2554,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       }
       __syncthreads();
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
-      if (a.k2flags & 256) {
-      } else if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
+      if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
           G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {
         // 4:2:0 (jdsample.c h2v2_fancy_upsample, as upsample_quad_h2v2): each
         // thread owns a pair of adjacent chroma columns (C, C + 1) and walks
@@ -2735,7 +2692,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       // (a row group is two whole waves: its rows are wave-uniform, so the
       // per-row tap read, cutout test and row changes are scalar)
       const int ya = __builtin_amdgcn_readfirstlane(oy0 + sub * half);
-      const int yb = __builtin_amdgcn_readfirstlane((a.k2flags & 512) ? ya : min(oy1, ya + half));
+      const int yb = __builtin_amdgcn_readfirstlane(min(oy1, ya + half));
       int ca = -1, cb = -1;
       uint32_t HA[6], HB[6];
       for (int dy = ya; dy < yb; dy++) {
@@ -2827,7 +2784,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   }
   const int roi_off = need;
   need += nrows * step;
-  const bool tiled = need <= LDS_BYTES && !(a.k2flags & 1);
+  const bool tiled = need <= LDS_BYTES;
   const bool staged = tiled || lut_b + nrows * step <= LDS_BYTES;  // (tap tables fit: see tabs)
   uint8_t *roi = lds + (tiled ? roi_off : lut_b);
   // Bands too wide for LDS stage their rows in the image's rgb slot at their
@@ -2835,7 +2792,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   // written with identical bytes by both.
   uint8_t *groi = a.arena + I.rgb_off;
   uint8_t *dst = staged ? roi : groi + (uint64_t)r0 * step;
-  const bool tabs = tap_b > 0 && lut_b <= LDS_BYTES / 2 && !(a.k2flags & 2);
+  const bool tabs = tap_b > 0 && lut_b <= LDS_BYTES / 2;
   if (tabs) {  // [0, out_w): columns, [out_w, out_w + rows): the band's rows
     for (int i = t; i < out_w + (oy1 - oy0); i += K2T) {
       if (P.kind == 2)
@@ -2859,10 +2816,8 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
     }
     __syncthreads();
     const bool q420 = ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 &&
-                      G.ve[1] == 2 && G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2 &&
-                      !(a.k2flags & 64);
-    if (a.k2flags & 8) {
-    } else if (q420) {  // one thread per chroma sample: a 2x2 quad of pixels
+                      G.ve[1] == 2 && G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2;
+    if (q420) {  // one thread per chroma sample: a 2x2 quad of pixels
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
       const int R0 = Y0 >> 1, C0 = X0 >> 1, qcols = (X1 >> 1) - C0 + 1;
       const int nq = ((Y1 >> 1) - R0 + 1) * qcols;
@@ -2911,7 +2866,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   // (resize.cpp VResizeLinearVec_32s8u).  Columns in the scalar tail
   // (>= vec_end) keep the per-pixel path.
   const int hoff = (((tiled ? roi_off : lut_b) + nrows * step) + 15) & ~15;
-  const bool sep = P.kind == 3 && staged && tabs && hoff + nrows * out_w * 8 <= LDS_BYTES && !(a.k2flags & 32);
+  const bool sep = P.kind == 3 && staged && tabs && hoff + nrows * out_w * 8 <= LDS_BYTES;
   uint2 *H = (uint2 *)(lds + hoff);
   __syncthreads();
   if (sep) {
@@ -2936,10 +2891,6 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       v[0] = ep.fill[0];
       v[1] = ep.fill[1];
       v[2] = ep.fill[2];
-    } else if (a.k2flags & 16) {
-      v[0] = lr.p[dx];
-      v[1] = lr.p[dx + 1];
-      v[2] = lr.p[dx + 2];
     } else if (sep && ep.src_x(dx) * 3 + 2 < P.vec_end) {
       const int cx = ep.src_x(dx);
       const LinTap ly = ltab[out_w + dy - oy0];
@@ -2966,7 +2917,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   };
   // pixel pairs: 12 bytes (fp16) / 6 bytes (u8) per thread, 4-/2-byte
   // aligned when rows and samples start aligned; single pixels otherwise
-  const bool pairs = (out_w & 1) == 0 && (a.out_stride & 3) == 0 && !(a.k2flags & 4);
+  const bool pairs = (out_w & 1) == 0 && (a.out_stride & 3) == 0;
   const int per = pairs ? 2 : 1;
   const int hw = out_w / per;
   const int npx = (oy1 - oy0) * hw;
@@ -3135,7 +3086,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   const int ri = I.ri, rj = I.rj, rw = I.rw;
   bool fast = P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && I.taps &&
               I.ncomp == 3 && !I.color_rgb && I.he[0] == 1 && I.ve[0] == 1 && I.he[1] == 2 && I.ve[1] == 2 &&
-              I.he[2] == 2 && I.ve[2] == 2 && I.cw[1] > 2 && I.cw[2] > 2 && !(a.k2flags & 128);
+              I.he[2] == 2 && I.ve[2] == 2 && I.cw[1] > 2 && I.cw[2] > 2;
   // LDS: band b + 1's tiles land in s_tile while band b's walk reads the
   // RGBx rows (sized for the workgroup's tallest band + the colour pass's
   // dummy word) in the dynamic area
@@ -3149,7 +3100,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   fast = fast && tiles_max <= K2L_TILE && rgb_off + rows_max * rw * 4 + 4 <= K2L_DYN;
   if (!fast) {  // the general path, one band after another
     for (int b = b0; b < b1; b++) {
-      k2_band<JM_RRC, FP16, true, K2L_DYN>(a, k, b, lds);
+      k2_band<JM_RRC, FP16, false, K2L_DYN>(a, k, b, lds);
       __syncthreads();
     }
     return;
@@ -3188,6 +3139,10 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   const uint32_t w0 = ((uint32_t)a0w << 4) | ((uint32_t)b0w << 20), w1 = ((uint32_t)a1w << 4) | ((uint32_t)b1w << 20);
   const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
   constexpr int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
+  // the counted wait below sets vmcnt's low field only (gfx9: 4 bits; the
+  // bits above it are expcnt / lgkmcnt); tests/test_isa_guards.py checks on
+  // the built code object that the walk issues exactly one store per row
+  static_assert(half > 0 && half < 16, "vmcnt(half) must fit the 4-bit field");
   // does this wave walk (hold a lane with an output column pair)?
   const bool wave_walks = ((t & ~63) % K2_COLS) < out_w / 2;
 
@@ -3386,7 +3341,6 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
 struct ffcv_jpeg_ctx {
   uint64_t *dbg;
   int diag_only;    // diagnostics (ffcv_jpeg_set_diag): kernels a launch runs
-  int diag_k2flags; // diagnostics: K2 timing-only flags
   int max_batch;
   uint32_t max_h, max_w;
   uint64_t max_bytes;
@@ -3507,9 +3461,10 @@ int ffcv_jpeg_set_debug(ffcv_jpeg_ctx *c, uint64_t *dbg) {
 // re-run on the previous launch's scratch) and K2 timing-only flags.  Set once per context, never
 // read from the environment on the launch path.
 int ffcv_jpeg_set_diag(ffcv_jpeg_ctx *c, int only, int k2flags) {
-  if (!c) return FFCV_EINVAL;
+  // (k2flags: the K2 timing-only switches of rounds 1-4 are gone from the
+  // product kernels; only 0 is accepted)
+  if (!c || k2flags != 0) return FFCV_EINVAL;
   c->diag_only = only ? only : 7;
-  c->diag_k2flags = k2flags;
   return FFCV_OK;
 }
 
@@ -3580,7 +3535,9 @@ int ffcv_jpeg_lane_table(ffcv_jpeg_ctx *c, void *stream, int n, uint32_t *blk0, 
 
 // Diagnostic hook (not in the public header): the arena reservation the last
 // launch's entropy kernel made for images [0, n) -- base offset and size in
-// bytes (size 0: the image reserved nothing) -- and the image record's status.
+// bytes (size 0: the image reserved nothing; K1 clears it for every image
+// before the parse) -- and the arena's capacity.  Statuses come from the
+// launch's own status array.
 int ffcv_jpeg_arena_regions(ffcv_jpeg_ctx *c, void *stream, int n, uint64_t *base, uint64_t *size,
                             uint64_t *capacity) {
   if (!c || n < 0 || n > c->max_batch || !base || !size) {
@@ -3652,7 +3609,6 @@ static JpegArgs make_args(ffcv_jpeg_ctx *c, const uint8_t *base, const ffcv_samp
   a.max_h = c->max_h;
   a.max_w = c->max_w;
   a.dbg = c->dbg;
-  a.k2flags = c->diag_k2flags;
   a.diag_only = c->diag_only;
   return a;
 }
@@ -3713,7 +3669,7 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[2], s));
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (!(only & 4)) {
-  } else if (batch >= c->k2_loop_min && !a.k2flags) {
+  } else if (batch >= c->k2_loop_min) {
     if (fp16)
       hipLaunchKernelGGL((jpeg_rrc_loop_kernel<true>), dim3((g2.x + K2L_BPW - 1) / K2L_BPW, batch), dim3(K2T),
                          K2L_DYN, s, a);

@@ -134,12 +134,6 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
   ep.fill[2] = p.cutout_fill[2];
   char *o = (char *)out + stride * k;
   const int out_w = p.out_w;
-#ifdef RRC_TIMING_SKIP_AREA
-  if (P.kind != 3) return;
-#endif
-#ifdef RRC_TIMING_SKIP_LINEAR
-  if (P.kind == 3) return;
-#endif
 
   // ---- stage the band's source rows into LDS
   int r0, r1;
@@ -160,11 +154,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
       for (int j = 0; j < RRC_STAGE_UNROLL; j++) {  // loads in flight before their LDS writes
         dst[j] = -1;
         v[j] = make_uint4(0, 0, 0, 0);
-#ifdef RRC_TIMING_NOSTAGE
-        if (false) {
-#else
         if (i0 + j * RRC_THREADS + t < n) {
-#endif
           const uint64_t ra = row0 + (uint64_t)r * src.step;
           // only chunks holding bytes of this row (none past the dataset's end)
           if (c < (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4)) {
@@ -281,9 +271,6 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
           sum = sum + bt[2] * NB[2][i];
           v[i] = sat_u8i(ffcv_f2i_rn(sum));
         }
-#ifdef RRC_TIMING_NOSTORE
-        if (p.cutout_fill[3] != 77) continue;  // timing only: compute without the stores
-#endif
         if (cm && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
 #pragma unroll
           for (int j = 0; j < 2; j++)
@@ -331,9 +318,6 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     for (int j = 0; j < 4; j++) cmask |= ep.in_cut(ep.cut_y, dx0 + j) ? 1u << j : 0u;
     // one 12-byte (u8) or three 8-byte (fp16) stores of the quad's pixels
     auto put = [&](int dy, int v[12]) {
-#ifdef RRC_TIMING_NOSTORE
-      if (p.cutout_fill[3] != 77) return;  // timing only: compute without the stores
-#endif
       if (cmask && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
 #pragma unroll
         for (int j = 0; j < 4; j++)

@@ -406,6 +406,8 @@ def main():
                     help='skip the later-epoch (entropy index) measurement reported beside the headline')
     ap.add_argument('--no-c5', action='store_true',
                     help='skip the C5 (raw, HBM-bound) and C2 sub-results the default C3 run reports beside its value')
+    ap.add_argument('--raw-no-ws', action='store_true',
+                    help='diagnostic A/B: raw path without the per-image plan / tap workspace (taps in every band)')
     ap.add_argument('--no-kernel-events', action='store_true',
                     help='do not record HIP events around each kernel of the timed launches (per-kernel roofline)')
     ap.add_argument('--parity-rows', type=int, default=1536,
@@ -517,6 +519,9 @@ def main():
                                   L.arena_for(hs, ws, sizes, cap))
                     if mode == 'jpg' else None),
             'used': 0,
+            # raw path: per-image plans + tap tables (ffcv_rrc_raw_batch_ws)
+            'ws': (torch.empty(L.rrc_raw_workspace_bytes(cap, out, out), dtype=torch.uint8, device=dev)
+                   if mode != 'jpg' and not args.raw_no_ws else None),
         })
     d_lut = None
     rp = L.RRCParams()
@@ -570,7 +575,8 @@ def main():
                 sl['dec'].rrc(d_data, sl['smp'], n, sl['crops'], sl['cut'], None, rp, sl['out'],
                               sl['status'], stream)
             else:
-                L.rrc_raw_batch(d_data, sl['smp'], n, sl['crops'], sl['cut'], None, rp, sl['out'], stream)
+                L.rrc_raw_batch(d_data, sl['smp'], n, sl['crops'], sl['cut'], None, rp, sl['out'], stream,
+                                workspace=sl['ws'])
         if ev is not None:
             ev[1].record(stream)
         return n
@@ -730,7 +736,8 @@ def main():
             L.gather_samples(d_table, ids, sl0['smp'], streams[0])
             L.draw_batch(ids, sl0['smp'], dp, sl0['crops'], sl0['cut'], None, sl0['rstat'], streams[0])
             ev0.record(streams[0])
-            L.rrc_raw_batch(d_data, sl0['smp'], cap, sl0['crops'], sl0['cut'], None, rp, sl0['out'], streams[0])
+            L.rrc_raw_batch(d_data, sl0['smp'], cap, sl0['crops'], sl0['cut'], None, rp, sl0['out'], streams[0],
+                            workspace=sl0['ws'])
             ev1.record(streams[0])
             streams[0].synchronize()
             raw_iso_ms += ev0.elapsed_time(ev1)

@@ -382,6 +382,22 @@ FFCV_HD LinTap lin_tap(double scale, double inv, int ssize, int d) {
   return t;
 }
 
+// Linear taps (resize.cpp linear coefficients, LinTap) packed in 8 bytes:
+// x = source index | border << 31, y = c0 | c1 << 16 (0 <= c0, c1 <= 2048).
+// Written once per image (K1 for JPEG, rrc_taps_kernel for raw samples) and
+// read by every band workgroup of the image.
+FFCV_DEV uint2 tap_pack(const LinTap &l) {
+  return make_uint2((uint32_t)l.s | ((uint32_t)l.border << 31), (uint32_t)(l.c0 & 0xffff) | ((uint32_t)l.c1 << 16));
+}
+FFCV_DEV LinTap tap_unpack(uint2 v) {
+  LinTap l;
+  l.s = (int)(v.x & 0x7fffffffu);
+  l.border = (int)(v.x >> 31);
+  l.c0 = (int)(int16_t)(v.y & 0xffff);
+  l.c1 = (int)(int16_t)(v.y >> 16);
+  return l;
+}
+
 // Source accessor: pixel (y, x) channel c of the ROI.
 struct RoiSrc {
   const uint8_t *p;

@@ -6,6 +6,7 @@
 //                    wrong: only the time or counters up to that point count)
 //   -DFFCV_K1_DIAG   K1's decode loops count their iterations (two
 //                    instructions per step) for tools/jpeg_phases.py
+//   -DRRC_STOP=n     the raw RRC kernel returns at hook n (wrong output)
 #pragma once
 
 #ifdef K1_STOP
@@ -23,4 +24,13 @@
 #define K1_DIAG(x) x
 #else
 #define K1_DIAG(x)
+#endif
+
+#ifdef RRC_STOP
+#define RRC_STOP_AT(n, cond, ...) \
+  if (RRC_STOP == (n) && (cond)) return __VA_ARGS__
+#else
+#define RRC_STOP_AT(n, cond, ...) \
+  do {                             \
+  } while (0)
 #endif

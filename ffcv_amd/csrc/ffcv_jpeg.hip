@@ -57,9 +57,11 @@
 #include "diag_hooks.h"
 
 #define JT 64           // lanes per wave
-// JL = 32 (two images per wave, each with twice the bits per lane) is
-// supported and bit-exact, but measured 35% slower than 64 in round 1: the
-// longer per-image latency outweighed the ~25% fewer sync lane-steps.
+// JL = 32 (two images per wave, each with twice the bits per lane) was
+// bit-exact in round 1 but 12-35% slower than 64 (the longer per-image latency
+// outweighed the ~25% fewer sync lane-steps); it is no longer maintained: a
+// round-5 build (-DJL=32, 46 KB of LDS, 3 workgroups per CU) ran the C3 bench
+// 10% slower and no longer matched the oracle (profiles/r5b_ab20_jl32.log).
 #ifndef JL
 #define JL 64           // lanes per image: a wave decodes JT / JL images side by side
 #endif
@@ -148,20 +150,7 @@ struct ImgInfo {
   uint64_t arena_base, arena_need;
 };
 
-// Linear taps (resize.cpp linear coefficients, LinTap) packed in 8 bytes:
-// x = source index | border << 31, y = c0 | c1 << 16 (0 <= c0, c1 <= 2048).
-#define K2_TAPS 512  // tap table entries per image: out_w + out_h <= 512
-FFCV_DEV uint2 tap_pack(const LinTap &l) {
-  return make_uint2((uint32_t)l.s | ((uint32_t)l.border << 31), (uint32_t)(l.c0 & 0xffff) | ((uint32_t)l.c1 << 16));
-}
-FFCV_DEV LinTap tap_unpack(uint2 v) {
-  LinTap l;
-  l.s = (int)(v.x & 0x7fffffffu);
-  l.border = (int)(v.x >> 31);
-  l.c0 = (int)(int16_t)(v.y & 0xffff);
-  l.c1 = (int)(int16_t)(v.y >> 16);
-  return l;
-}
+#define K2_TAPS 512  // tap table entries per image: out_w + out_h <= 512 (tap_pack format)
 
 // Huffman decode tables built from one image's DHT segments.  K1 runs JW
 // images per workgroup; images whose tables (and table slots) are byte-

@@ -9,6 +9,7 @@
 // reads each crop ROI once and writes the final (u8 or fp16) pixels once.
 #include "api_internal.h"
 #include "device_common.h"
+#include "diag_hooks.h"
 
 // ------------------------------------------------------------ draws -------
 __global__ void __launch_bounds__(64) draw_kernel(const uint64_t *__restrict__ ids,
@@ -86,6 +87,8 @@ struct LdsSrc {
 //   writes one contiguous run of the output row.
 //   Otherwise (area downscale, copy, widths not a multiple of 4): the
 //   per-pixel restatement, over the staged rows when they fit.
+// rrc_taps_kernel's table: entries per image (even: 16-byte quads stay aligned)
+#define RAW_TAPS(p) (((p).out_w + (p).out_h + 1) & ~1)
 #ifndef RRC_WPE
 #define RRC_WPE 5  // waves per SIMD the raw kernel is compiled for (5 workgroups per CU by LDS)
 #endif
@@ -105,7 +108,8 @@ template <bool FP16>
 FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
                        const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
                        const uint8_t *__restrict__ flips, const ffcv_rrc_params &p, uint64_t stride,
-                       void *__restrict__ out, const int k, const int band, RrcLds<FP16> &S) {
+                       void *__restrict__ out, const int k, const int band, RrcLds<FP16> &S,
+                       const ResizePlan *__restrict__ plans, const uint2 *__restrict__ taps) {
   uint16_t *s_lut = S.lut;
   uint4 *s_src = S.src;
   uint4 *s_rt = S.rt;
@@ -120,7 +124,12 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
   if (oy0 >= p.out_h) return;
   const int ci = crops[4 * k], cj = crops[4 * k + 1], chh = crops[4 * k + 2], cww = crops[4 * k + 3];
   GlobalSrc src{base + s.offset + ((uint64_t)ci * s.width + cj) * 3, (uint64_t)s.width * 3};
-  ResizePlan P = make_plan(cww, chh, p.out_w, p.out_h);
+  // the image's plan and linear taps from rrc_taps_kernel when the caller gave
+  // a workspace (computed once per image, not in each of its band workgroups:
+  // the f64 plan and four column taps per thread were a third of this
+  // kernel's instructions, profiles/r5c_c5parts.txt)
+  const uint2 *itaps = taps ? taps + (uint64_t)k * RAW_TAPS(p) : nullptr;
+  ResizePlan P = plans ? plans[k] : make_plan(cww, chh, p.out_w, p.out_h);
   Epilogue ep;
   ep.out_h = p.out_h;
   ep.out_w = p.out_w;
@@ -135,6 +144,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
   char *o = (char *)out + stride * k;
   const int out_w = p.out_w;
 
+  RRC_STOP_AT(1, p.cutout_fill[3] != 77);  // diagnostics: the band's set-up only
   // ---- stage the band's source rows into LDS
   int r0, r1;
   band_rows(P, oy0, oy1, &r0, &r1);
@@ -175,12 +185,13 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     }
   }
   if (P.kind == 3 && t < oy1 - oy0) {  // clamped source rows, weights << 8: no per-row clamps in the walk
-    const LinTap l = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+    const LinTap l = itaps ? tap_unpack(itaps[p.out_w + oy0 + t]) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
     s_rt[t] = make_uint4((uint32_t)min(max(l.s, 0), P.sh - 1), (uint32_t)min(max(l.s + 1, 0), P.sh - 1),
                          ((uint32_t)l.c0 & 0xfffu) << 8, ((uint32_t)l.c1 & 0xfffu) << 8);
   }
   if (P.kind == 2 && t < oy1 - oy0) s_at[t] = area_taps(P.sh, P.scale_y, oy0 + t);
   __syncthreads();
+  RRC_STOP_AT(2, p.cutout_fill[3] != 77);  // diagnostics: set-up + staging
 
   const bool aligned4 = ((((uintptr_t)out) | stride) & 3) == 0;
   const int nq = out_w >> 2;  // column quads
@@ -361,9 +372,16 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
       return;
     }
     int xa[4], xb[4], wa[4], wb[4];
+    uint4 tq0 = make_uint4(0, 0, 0, 0), tq1 = tq0;
+    if (itaps) {  // the quad's four column taps (flip applied): 32 bytes
+      tq0 = *(const uint4 *)(itaps + dx0);
+      tq1 = *(const uint4 *)(itaps + dx0 + 2);
+    }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const LinTap l = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + j));
+      const uint4 &tq = j < 2 ? tq0 : tq1;
+      const LinTap l = itaps ? tap_unpack((j & 1) ? make_uint2(tq.z, tq.w) : make_uint2(tq.x, tq.y))
+                             : lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + j));
       // a border tap (src[s] * 2048) as the two-tap form with weights (2048, 0)
       xa[j] = 3 * l.s;
       xb[j] = 3 * (l.border ? l.s : l.s + 1);
@@ -389,6 +407,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     auto mulhi24 = [](uint32_t a, uint32_t b) -> uint32_t {  // a, b < 2^24: v_mul_hi_u32_u24
       return (uint32_t)(((uint64_t)(a & 0xffffffu) * (b & 0xffffffu)) >> 32);
     };
+    RRC_STOP_AT(3, p.cutout_fill[3] != 77);  // diagnostics: + the linear walk's column taps
     int ca = -1, cb = -1;
     uint32_t HA[12], HB[12];
     for (int dy = gy0; dy < gy1; dy++) {
@@ -438,9 +457,31 @@ __global__ void __launch_bounds__(RRC_THREADS) __attribute__((amdgpu_waves_per_e
     rrc_raw_kernel(const uint8_t *__restrict__ base, const ffcv_sample *__restrict__ samples,
                    const int32_t *__restrict__ crops, const int32_t *__restrict__ cut,
                    const uint8_t *__restrict__ flips, ffcv_rrc_params p, uint64_t stride,
-                   void *__restrict__ out) {
+                   void *__restrict__ out, const ResizePlan *__restrict__ plans, const uint2 *__restrict__ taps) {
   __shared__ RrcLds<FP16> S;
-  rrc_band<FP16>(base, samples, crops, cut, flips, p, stride, out, (int)blockIdx.y, (int)blockIdx.x, S);
+  rrc_band<FP16>(base, samples, crops, cut, flips, p, stride, out, (int)blockIdx.y, (int)blockIdx.x, S, plans,
+                 taps);
+}
+
+// Per-image resize plan + linear tap table for rrc_raw_kernel (one thread per
+// tap: columns [0, out_w) with the image's flip applied, then rows [out_w,
+// out_w + out_h)), the same functions the band workgroups would evaluate
+// (resize.cpp linear coefficients, make_plan), so the output is unchanged.
+__global__ void __launch_bounds__(256) rrc_taps_kernel(const int32_t *__restrict__ crops,
+                                                       const uint8_t *__restrict__ flips, ffcv_rrc_params p,
+                                                       ResizePlan *__restrict__ plans, uint2 *__restrict__ taps) {
+  const int k = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  const ResizePlan P = make_plan(crops[4 * k + 3], crops[4 * k + 2], p.out_w, p.out_h);
+  if (i == 0) plans[k] = P;
+  if (P.kind != 3 || i >= p.out_w + p.out_h) return;
+  LinTap l;
+  if (i < p.out_w) {
+    const int flip = flips ? flips[k] : 0;
+    l = lin_tap(P.scale_x, P.inv_x, P.sw, flip ? p.out_w - 1 - i : i);
+  } else {
+    l = lin_tap(P.scale_y, P.inv_y, P.sh, i - p.out_w);
+  }
+  taps[(uint64_t)k * RAW_TAPS(p) + i] = tap_pack(l);
 }
 
 // --------------------------------------------- simple (raw) gather -------
@@ -567,26 +608,59 @@ int ffcv_draw_batch(void *stream, const uint64_t *sample_ids, const ffcv_sample 
   return FFCV_OK;
 }
 
-int ffcv_rrc_raw_batch(void *stream, const uint8_t *base, const ffcv_sample *samples, int batch,
-                       const int32_t *crops, const int32_t *cutout_yx, const uint8_t *flips,
-                       const ffcv_rrc_params *p, void *out) {
+static uint64_t raw_plans_bytes(int batch) { return ((uint64_t)batch * sizeof(ResizePlan) + 255) & ~(uint64_t)255; }
+
+uint64_t ffcv_rrc_raw_workspace_bytes(int batch, int out_h, int out_w) {
+  if (batch <= 0 || out_h <= 0 || out_w <= 0) return 0;
+  ffcv_rrc_params q{};
+  q.out_h = out_h;
+  q.out_w = out_w;
+  return raw_plans_bytes(batch) + (uint64_t)batch * RAW_TAPS(q) * sizeof(uint2);
+}
+
+int ffcv_rrc_raw_batch_ws(void *stream, const uint8_t *base, const ffcv_sample *samples, int batch,
+                          const int32_t *crops, const int32_t *cutout_yx, const uint8_t *flips,
+                          const ffcv_rrc_params *p, void *out, void *workspace, uint64_t workspace_bytes) {
   if (batch < 0 || !p || !base || !samples || !crops || !out || p->out_h <= 0 || p->out_w <= 0) {
     ffcv::set_error("ffcv_rrc_raw_batch: invalid arguments");
     return FFCV_EINVAL;
   }
   if (batch == 0) return FFCV_OK;
+  const ResizePlan *plans = nullptr;
+  const uint2 *taps = nullptr;
+  if (workspace) {
+    const uint64_t need = ffcv_rrc_raw_workspace_bytes(batch, p->out_h, p->out_w);
+    if (workspace_bytes < need || ((uintptr_t)workspace & 15)) {
+      ffcv::set_error("ffcv_rrc_raw_batch_ws: workspace of %llu bytes (16-byte aligned) needed, got %llu",
+                      (unsigned long long)need, (unsigned long long)workspace_bytes);
+      return FFCV_EINVAL;
+    }
+    ResizePlan *wp = (ResizePlan *)workspace;
+    uint2 *wt = (uint2 *)((uint8_t *)workspace + raw_plans_bytes(batch));
+    hipLaunchKernelGGL(rrc_taps_kernel, dim3((p->out_w + p->out_h + 255) / 256, batch), dim3(256), 0,
+                       ffcv::as_stream(stream), crops, flips, *p, wp, wt);
+    FFCV_LAUNCH_CHECK("rrc_taps_kernel");
+    plans = wp;
+    taps = wt;
+  }
   const bool fp16 = p->lut != nullptr;
   uint64_t dense = (uint64_t)p->out_h * p->out_w * 3 * (fp16 ? 2 : 1);
   uint64_t stride = p->out_stride ? p->out_stride : dense;
   dim3 grid((p->out_h + RRC_BAND - 1) / RRC_BAND, batch);
   if (fp16)
     hipLaunchKernelGGL(rrc_raw_kernel<true>, grid, dim3(RRC_THREADS), 0, ffcv::as_stream(stream), base,
-                       samples, crops, cutout_yx, flips, *p, stride, out);
+                       samples, crops, cutout_yx, flips, *p, stride, out, plans, taps);
   else
     hipLaunchKernelGGL(rrc_raw_kernel<false>, grid, dim3(RRC_THREADS), 0, ffcv::as_stream(stream), base,
-                       samples, crops, cutout_yx, flips, *p, stride, out);
+                       samples, crops, cutout_yx, flips, *p, stride, out, plans, taps);
   FFCV_LAUNCH_CHECK("rrc_raw_kernel");
   return FFCV_OK;
+}
+
+int ffcv_rrc_raw_batch(void *stream, const uint8_t *base, const ffcv_sample *samples, int batch,
+                       const int32_t *crops, const int32_t *cutout_yx, const uint8_t *flips,
+                       const ffcv_rrc_params *p, void *out) {
+  return ffcv_rrc_raw_batch_ws(stream, base, samples, batch, crops, cutout_yx, flips, p, out, nullptr, 0);
 }
 
 int ffcv_gather_samples(void *stream, const ffcv_sample *table, uint64_t n_table, const uint64_t *ids,

@@ -331,14 +331,16 @@ class ResizedCropRGBImageDecoder(SimpleRGBImageDecoder, metaclass=ABCMeta):
                 ss.check_status(status[:B], type(self).__name__)
                 if ss.any_mode(f_ix, 1):
                     L.rrc_raw_batch(ss.data, smp[:B], B, crops, cyx if cut is not None else None,
-                                    flips if use_flip else None, rp, out, stream)
+                                    flips if use_flip else None, rp, out, stream,
+                                    workspace=ss.raw_workspace(f_ix, rp.out_h, rp.out_w))
                 return out[:B]
             samples = ss.batch_samples(f_ix, smp)
             L.draw_batch(ss.batch_ids, samples, dp, crops, cyx if cut is not None else None,
                          flips if use_flip else None, None, stream)
             if ss.any_mode(f_ix, 1):
                 L.rrc_raw_batch(ss.data, samples, B, crops, cyx if cut is not None else None,
-                                flips if use_flip else None, rp, out, stream)
+                                flips if use_flip else None, rp, out, stream,
+                                workspace=ss.raw_workspace(f_ix, rp.out_h, rp.out_w))
             if ss.any_mode(f_ix, 0):
                 dec = ss.jpeg_decoder(f_ix)
                 dec.rrc(ss.data, samples, B, crops, cyx if cut is not None else None,

@@ -88,6 +88,9 @@ _SIGS = {
                                      c_void_p]),
     'ffcv_rrc_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
+    'ffcv_rrc_raw_batch_ws': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]),
+    'ffcv_rrc_raw_workspace_bytes': (c_uint64, [c_int, c_int, c_int]),
     'ffcv_gather_samples': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_int, c_void_p]),
     'ffcv_gather_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_uint64]),
     'ffcv_jpeg_create': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64]),
@@ -305,8 +308,22 @@ def gather_samples(table, ids, out, stream=None):
                                      int(ids.shape[0]), _p(out)), 'ffcv_gather_samples')
 
 
+def rrc_raw_workspace_bytes(batch, out_h, out_w):
+    """Device bytes rrc_raw_batch's workspace needs (per-image plan + taps)."""
+    return int(lib().ffcv_rrc_raw_workspace_bytes(int(batch), int(out_h), int(out_w)))
+
+
 def rrc_raw_batch(base, samples, batch, crops, cutout_yx, flips, params: RRCParams, out,
-                  stream=None):
+                  stream=None, workspace=None):
+    """Raw-mode RRC (+ cutout / flip / LUT).  With a device uint8 `workspace`
+    of rrc_raw_workspace_bytes() the per-image plans and tap tables are
+    computed once per image (ffcv_rrc_raw_batch_ws); output is identical."""
+    if workspace is not None:
+        _check(lib().ffcv_rrc_raw_batch_ws(_stream(stream), _p(base), _p(samples), int(batch),
+                                           _p(crops), _p(cutout_yx), _p(flips), ctypes.byref(params),
+                                           _p(out), _p(workspace), int(workspace.numel())),
+               'ffcv_rrc_raw_batch_ws')
+        return
     _check(lib().ffcv_rrc_raw_batch(_stream(stream), _p(base), _p(samples), int(batch),
                                     _p(crops), _p(cutout_yx), _p(flips), ctypes.byref(params),
                                     _p(out)), 'ffcv_rrc_raw_batch')

@@ -249,5 +249,17 @@ class BatchContext:
             self._decoders[f_ix] = dec
         return self._decoders[f_ix]
 
+    def raw_workspace(self, f_ix, out_h, out_w):
+        """Device workspace of this slot for the raw decoder's per-image plans
+        and tap tables (ffcv_rrc_raw_batch_ws), one per (field, output size)."""
+        from .. import libffcv as L
+        key = ('raw_ws', f_ix, out_h, out_w)
+        ws = self._staging.get(key)
+        if ws is None:
+            ws = ch.empty(L.rrc_raw_workspace_bytes(self.batch_size, out_h, out_w), dtype=ch.uint8,
+                          device=self.dataset.device)
+            self._staging[key] = ws
+        return ws
+
     def check_status(self, status, what):
         self.pending_status.append((status, what))

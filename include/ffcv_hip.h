@@ -217,6 +217,20 @@ int ffcv_rrc_raw_batch(void *stream, const uint8_t *base,
                        const uint8_t *flips, const ffcv_rrc_params *p,
                        void *out);
 
+/* The same with a caller-provided device workspace (16-byte aligned, at
+ * least ffcv_rrc_raw_workspace_bytes(batch, out_h, out_w) bytes; NULL runs
+ * ffcv_rrc_raw_batch): each image's resize plan and linear tap table are
+ * computed once (one small kernel, one thread per tap) instead of in every
+ * band workgroup of the image.  Output is identical.  The workspace is
+ * overwritten by the launch and must not be shared by launches in flight
+ * on different streams. */
+int ffcv_rrc_raw_batch_ws(void *stream, const uint8_t *base,
+                          const ffcv_sample *samples, int batch,
+                          const int32_t *crops, const int32_t *cutout_yx,
+                          const uint8_t *flips, const ffcv_rrc_params *p,
+                          void *out, void *workspace, uint64_t workspace_bytes);
+uint64_t ffcv_rrc_raw_workspace_bytes(int batch, int out_h, int out_w);
+
 /* Per-batch descriptor gather: out[k] = table[ids[k]] (the reference reads
  * metadata[source_ix] per sample, rgb_image.py:188-189).  table: device
  * ffcv_sample[N] built once per dataset; ids: device uint64[B]. */

@@ -116,7 +116,13 @@ def _run_raw_rrc(hip_lib, imgs, crops, out_hw, cut=None, cut_size=0, fill=(0, 0,
     else:
         out = torch.zeros((B, out_hw[0], out_hw[1], 3), dtype=torch.uint8, device='cuda:0')
     L.rrc_raw_batch(d_buf, d_smp, B, d_crops, d_cut, d_flips, p, out)
+    # the per-image plan / tap table path (ffcv_rrc_raw_batch_ws) must write
+    # the same bytes
+    ws = torch.empty(L.rrc_raw_workspace_bytes(B, *out_hw), dtype=torch.uint8, device='cuda:0')
+    out_ws = torch.full_like(out, 7)
+    L.rrc_raw_batch(d_buf, d_smp, B, d_crops, d_cut, d_flips, p, out_ws, workspace=ws)
     torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.uint8), out_ws.view(torch.uint8)), 'workspace path differs'
     return out.cpu().numpy()
 
 

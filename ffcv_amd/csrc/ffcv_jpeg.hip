@@ -2255,12 +2255,24 @@ struct ColorGeom {
 // record where they are used issued them in ~6 dependent round trips (the
 // compiler may not hoist loads above the status / mode branches), which was
 // most of K2's per-workgroup fixed cost.
+// Round 5: the head read through the scalar cache instead (s_load: no
+// v_readlane per field, 49 VALU per wave; K2REC_SMEM=0 restores the vector
+// load + broadcast for A/B runs).
 #define K2REC_DW ((int)((offsetof(ImgInfo, taps) + 4) / 4))
 static_assert(K2REC_DW <= 64, "record head fits one wave's lanes");
+#ifndef K2REC_SMEM
+#define K2REC_SMEM 1
+#endif
 struct K2Rec {
+#if K2REC_SMEM
+  const __attribute__((address_space(4))) uint32_t *p;  // the record (written by K1: a previous kernel)
+  FFCV_DEV void load(const ImgInfo *rec, int) { p = (const __attribute__((address_space(4))) uint32_t *)rec; }
+  FFCV_DEV uint32_t u(int i) const { return p[i]; }
+#else
   uint32_t w;  // this lane's dword of the record head
   FFCV_DEV void load(const ImgInfo *rec, int t) { w = (t & 63) < K2REC_DW ? ((const uint32_t *)rec)[t & 63] : 0u; }
   FFCV_DEV uint32_t u(int i) const { return (uint32_t)__builtin_amdgcn_readlane((int)w, i); }
+#endif
   FFCV_DEV int32_t s(int i) const { return (int32_t)u(i); }
   FFCV_DEV uint64_t u64(int i) const { return (uint64_t)u(i) | ((uint64_t)u(i + 1) << 32); }
   FFCV_DEV double f64(int i) const { return __builtin_bit_cast(double, u64(i)); }

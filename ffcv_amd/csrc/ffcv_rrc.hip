@@ -184,8 +184,8 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         if (dst[j] >= 0) s_src[dst[j]] = v[j];
     }
   }
-  if (P.kind == 3 && t < oy1 - oy0) {  // clamped source rows, weights << 8: no per-row clamps in the walk
-    const LinTap l = itaps ? tap_unpack(itaps[p.out_w + oy0 + t]) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+  if (P.kind == 3 && !itaps && t < oy1 - oy0) {  // clamped source rows, weights << 8: no per-row clamps in the walk
+    const LinTap l = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
     s_rt[t] = make_uint4((uint32_t)min(max(l.s, 0), P.sh - 1), (uint32_t)min(max(l.s + 1, 0), P.sh - 1),
                          ((uint32_t)l.c0 & 0xfffu) << 8, ((uint32_t)l.c1 & 0xfffu) << 8);
   }
@@ -408,30 +408,114 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
       return (uint32_t)(((uint64_t)(a & 0xffffffu) * (b & 0xffffffu)) >> 32);
     };
     RRC_STOP_AT(3, p.cutout_fill[3] != 77);  // diagnostics: + the linear walk's column taps
-    int ca = -1, cb = -1;
-    uint32_t HA[12], HB[12];
-    for (int dy = gy0; dy < gy1; dy++) {
-      const uint4 ly = s_rt[dy - oy0];
-      const int ra = (int)ly.x, rb = (int)ly.y;
-      if (ra != ca) {
-        if (ra == cb) {
+    // row taps: from the image's table through the scalar cache (the rows of a
+    // row group are wave-uniform) when there is one, else the band's LDS records
+    const __attribute__((address_space(4))) uint32_t *rtp =
+        itaps ? (const __attribute__((address_space(4))) uint32_t *)(itaps + out_w) : nullptr;
+    // the two source rows' horizontal sums live in register sets X and Y;
+    // which one is the upper row (A) flips when the walk moves down one
+    // source row, instead of copying B into A (12 moves per such row): the
+    // flag is wave-uniform, so both orders are separate straight-line code
+    uint32_t HX[12], HY[12];
+    int cx = -1, cy = -1;  // source rows held by X / Y
+    bool par = false;      // false: A = X, B = Y
+    auto emit = [&](int dy, const uint32_t (&A)[12], const uint32_t (&B)[12], uint32_t c0, uint32_t c1) {
+      if (FP16) {
+        int v[12];
 #pragma unroll
-          for (int i = 0; i < 12; i++) HA[i] = HB[i];
-        } else {
-          hrow(ra, HA);
+        for (int i = 0; i < 12; i++)  // VResizeLinearVec_32s8u: (m0 + 2 + m1) >> 2, no saturation (see hrow)
+          v[i] = (int)((mulhi24(A[i], c0) + mulhi24(B[i], c1) + 2u) >> 2);
+        put(dy, v);
+      } else {
+        // u8: t = m0 + m1 + 2 (<= 1022) per value, two values per dword in
+        // 16-bit lanes, one packed shift (v_pk_lshrrev_b16) per pair and the
+        // low bytes picked by one v_perm per output dword: 5 instructions per
+        // dword instead of 8 (a cutout value is fill << 2: exact after >> 2)
+        uint32_t tv[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) tv[i] = mulhi24(A[i], c0) + mulhi24(B[i], c1) + 2u;
+        if (cmask && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if ((cmask >> j) & 1) {
+              tv[3 * j] = (uint32_t)ep.fill[0] << 2;
+              tv[3 * j + 1] = (uint32_t)ep.fill[1] << 2;
+              tv[3 * j + 2] = (uint32_t)ep.fill[2] << 2;
+            }
         }
-        ca = ra;
-      }
-      if (rb != cb) {
-        hrow(rb, HB);
-        cb = rb;
-      }
-      const uint32_t c0 = ly.z, c1 = ly.w;
-      int v[12];
+        auto shr2 = [](uint32_t x) -> uint32_t {  // both 16-bit halves >> 2
+          return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, x) >> (u16x2_t){2, 2});
+        };
+        typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+        uint32_t wd[3];
 #pragma unroll
-      for (int i = 0; i < 12; i++)  // VResizeLinearVec_32s8u: (m0 + 2 + m1) >> 2, no saturation (see hrow)
-        v[i] = (int)((mulhi24(HA[i], c0) + mulhi24(HB[i], c1) + 2u) >> 2);
-      put(dy, v);
+        for (int d = 0; d < 3; d++) {
+          const uint32_t lo = shr2(tv[4 * d] | (tv[4 * d + 1] << 16)), hi = shr2(tv[4 * d + 2] | (tv[4 * d + 3] << 16));
+          wd[d] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);  // bytes lo.0, lo.2, hi.0, hi.2
+        }
+        u32x3 w;
+        w.x = wd[0];
+        w.y = wd[1];
+        w.z = wd[2];
+        __builtin_nontemporal_store(w, (u32x3 *)((uint8_t *)o + ((uint64_t)dy * out_w + dx0) * 3));
+      }
+    };
+    for (int dy = gy0; dy < gy1; dy++) {
+      int ra, rb;
+      uint32_t c0, c1;
+      if (rtp) {
+        const uint32_t tx = rtp[2 * dy], ty = rtp[2 * dy + 1];
+        const int sr = (int)(tx & 0x7fffffffu);
+        ra = min(max(sr, 0), P.sh - 1);
+        rb = min(max(sr + 1, 0), P.sh - 1);
+        c0 = (ty & 0xfffu) << 8;
+        c1 = ((ty >> 16) & 0xfffu) << 8;
+      } else {
+        const uint4 ly = s_rt[dy - oy0];
+        ra = (int)ly.x;
+        rb = (int)ly.y;
+        c0 = ly.z;
+        c1 = ly.w;
+      }
+      if (!par) {  // A = X, B = Y
+        if (ra != cx && ra == cy) {  // down one source row: Y is the new A, X takes the new B
+          par = true;
+          if (rb != cx) {
+            hrow(rb, HX);
+            cx = rb;
+          }
+        } else {
+          if (ra != cx) {
+            hrow(ra, HX);
+            cx = ra;
+          }
+          if (rb != cy) {
+            hrow(rb, HY);
+            cy = rb;
+          }
+        }
+      } else {  // A = Y, B = X
+        if (ra != cy && ra == cx) {
+          par = false;
+          if (rb != cy) {
+            hrow(rb, HY);
+            cy = rb;
+          }
+        } else {
+          if (ra != cy) {
+            hrow(ra, HY);
+            cy = ra;
+          }
+          if (rb != cx) {
+            hrow(rb, HX);
+            cx = rb;
+          }
+        }
+      }
+      if (par)
+        emit(dy, HY, HX, c0, c1);
+      else
+        emit(dy, HX, HY, c0, c1);
     }
     return;
   }

@@ -52,8 +52,8 @@ FFCV_DEV void store_px(void *out, uint64_t idx, const int v[3], const uint16_t *
 #ifndef RRC_BAND
 #define RRC_BAND 16  // output rows per workgroup
 #endif
-#ifndef RRC_STAGE_UNROLL
-#define RRC_STAGE_UNROLL 8  // 16-byte loads in flight per thread while staging
+#ifndef RRC_STAGE_ROWS
+#define RRC_STAGE_ROWS 5  // rows a wave stages per batch of loads in flight (2 x 16 B per lane each)
 #endif
 #ifndef RRC_LDS_BYTES
 #define RRC_LDS_BYTES 30464  // source-row stage: the most that keeps 5 workgroups per CU with the LUT and tap tables (28 KB: 1% slower, 24 KB: 15% slower)
@@ -154,35 +154,33 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
   const bool staged = nrows * nch * 16 <= RRC_LDS_BYTES;
   LdsSrc L{(const uint8_t *)s_src, nch * 16, (int)(row0 & 15), (int)(src.step & 15), r0};
   if (staged) {
-    const int n = nrows * nch;
-    int r = t / nch, c = t - r * nch;
-    const int dr = RRC_THREADS / nch, dc = RRC_THREADS - dr * nch;
-    for (int i0 = 0; i0 < n; i0 += RRC_THREADS * RRC_STAGE_UNROLL) {
-      uint4 v[RRC_STAGE_UNROLL];
-      int dst[RRC_STAGE_UNROLL];
+    // wave w copies rows w, w + 4, ...; lane l the row's 16-byte chunks l and
+    // l + 64: the row address and its chunk count are wave-uniform (scalar),
+    // a lane's chunk offset is fixed, and a wave has up to RRC_STAGE_ROWS
+    // rows' loads in flight before its LDS writes
+    const int wv = t >> 6, ln = t & 63;
+    for (int cg = 0; cg < nch; cg += 128)  // (one pass for rows up to 2 KB: crops up to 677 px wide)
+      for (int rb0 = wv; rb0 < nrows; rb0 += 4 * RRC_STAGE_ROWS) {
+        uint4 v[RRC_STAGE_ROWS][2];
 #pragma unroll
-      for (int j = 0; j < RRC_STAGE_UNROLL; j++) {  // loads in flight before their LDS writes
-        dst[j] = -1;
-        v[j] = make_uint4(0, 0, 0, 0);
-        if (i0 + j * RRC_THREADS + t < n) {
+        for (int q = 0; q < RRC_STAGE_ROWS; q++) {
+          const int r = rb0 + 4 * q;
           const uint64_t ra = row0 + (uint64_t)r * src.step;
-          // only chunks holding bytes of this row (none past the dataset's end)
-          if (c < (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4)) {
-            v[j] = *(const uint4 *)(uintptr_t)((ra & ~(uint64_t)15) + 16 * (uint64_t)c);
-            dst[j] = r * nch + c;
-          }
+          // chunks holding bytes of this row (none past the dataset's end)
+          const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
+          const uint4 *rp = (const uint4 *)(uintptr_t)(ra & ~(uint64_t)15) + cg;
+          v[q][0] = ln < lim ? rp[ln] : make_uint4(0, 0, 0, 0);
+          v[q][1] = ln + 64 < lim ? rp[ln + 64] : make_uint4(0, 0, 0, 0);
         }
-        c += dc;
-        r += dr;
-        if (c >= nch) {
-          c -= nch;
-          r++;
+#pragma unroll
+        for (int q = 0; q < RRC_STAGE_ROWS; q++) {
+          const int r = rb0 + 4 * q;
+          const uint64_t ra = row0 + (uint64_t)r * src.step;
+          const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
+          if (ln < lim) s_src[r * nch + cg + ln] = v[q][0];
+          if (ln + 64 < lim) s_src[r * nch + cg + ln + 64] = v[q][1];
         }
       }
-#pragma unroll
-      for (int j = 0; j < RRC_STAGE_UNROLL; j++)
-        if (dst[j] >= 0) s_src[dst[j]] = v[j];
-    }
   }
   if (P.kind == 3 && !itaps && t < oy1 - oy0) {  // clamped source rows, weights << 8: no per-row clamps in the walk
     const LinTap l = lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);

@@ -7,6 +7,7 @@
 //   -DFFCV_K1_DIAG   K1's decode loops count their iterations (two
 //                    instructions per step) for tools/jpeg_phases.py
 //   -DRRC_STOP=n     the raw RRC kernel returns at hook n (wrong output)
+//   -DK2_STOP=n      the per-band K2's linear fast path returns at hook n
 #pragma once
 
 #ifdef K1_STOP
@@ -32,5 +33,14 @@
 #else
 #define RRC_STOP_AT(n, cond, ...) \
   do {                             \
+  } while (0)
+#endif
+
+#ifdef K2_STOP
+#define K2_STOP_AT(n, cond, ...) \
+  if (K2_STOP == (n) && (cond)) return __VA_ARGS__
+#else
+#define K2_STOP_AT(n, cond, ...) \
+  do {                            \
   } while (0)
 #endif

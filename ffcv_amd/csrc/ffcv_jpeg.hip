@@ -2516,6 +2516,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
     const int rgb_off = need;
     need += nrows * rw * 4 + 4;  // + a dummy word for the colour pass's off-crop pixels
     if (need <= LDS_BYTES) {
+      K2_STOP_AT(1, a.out_stride != 77);  // diagnostics: the band's set-up (record, LUT, taps, tile bounds)
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
       if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
       TPlane tp[3];
@@ -2554,6 +2555,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
         tp[c] = TPlane{(const uint8_t *)tl, ty0[c], tx0[c], tpitch[c]};
       }
       __syncthreads();
+      K2_STOP_AT(2, a.out_stride != 77);  // diagnostics: + the plane tiles
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
       if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
           G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {
@@ -2638,6 +2640,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
         }
       }
       __syncthreads();
+      K2_STOP_AT(3, a.out_stride != 77);  // diagnostics: + the colour pass
       const int tx = t % K2_COLS, sub = t / K2_COLS;
       if (tx >= out_w / 2) return;
       const int dx0 = 2 * tx;

@@ -416,7 +416,6 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     // flag is wave-uniform, so both orders are separate straight-line code
     uint32_t HX[12], HY[12];
     int cx = -1, cy = -1;  // source rows held by X / Y
-    bool par = false;      // false: A = X, B = Y
     auto emit = [&](int dy, const uint32_t (&A)[12], const uint32_t (&B)[12], uint32_t c0, uint32_t c1) {
       if (FP16) {
         int v[12];
@@ -455,12 +454,17 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         w.x = wd[0];
         w.y = wd[1];
         w.z = wd[2];
-        __builtin_nontemporal_store(w, (u32x3 *)((uint8_t *)o + ((uint64_t)dy * out_w + dx0) * 3));
+        // uniform row address (scalar) + this lane's 32-bit offset: the
+        // store's saddr form, no 64-bit address arithmetic per row
+        typedef __attribute__((address_space(1))) uint8_t gbyte_t;
+        typedef __attribute__((address_space(1))) u32x3 gu32x3_t;
+        const uint64_t ra64 = (uint64_t)(uintptr_t)o + (uint64_t)(uint32_t)dy * (uint32_t)(3 * out_w);
+        gbyte_t *orow = (gbyte_t *)(uintptr_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ra64 >> 32)) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ra64));
+        __builtin_nontemporal_store(w, (gu32x3_t *)(orow + (uint32_t)(3 * dx0)));
       }
     };
-    for (int dy = gy0; dy < gy1; dy++) {
-      int ra, rb;
-      uint32_t c0, c1;
+    auto row_taps = [&](int dy, int &ra, int &rb, uint32_t &c0, uint32_t &c1) {
       if (rtp) {
         const uint32_t tx = rtp[2 * dy], ty = rtp[2 * dy + 1];
         const int sr = (int)(tx & 0x7fffffffu);
@@ -475,45 +479,41 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         c0 = ly.z;
         c1 = ly.w;
       }
-      if (!par) {  // A = X, B = Y
-        if (ra != cx && ra == cy) {  // down one source row: Y is the new A, X takes the new B
-          par = true;
-          if (rb != cx) {
-            hrow(rb, HX);
-            cx = rb;
-          }
-        } else {
-          if (ra != cx) {
-            hrow(ra, HX);
-            cx = ra;
-          }
-          if (rb != cy) {
-            hrow(rb, HY);
-            cy = rb;
-          }
+    };
+    // two loops, one per role assignment (a single loop with a role flag was
+    // compiled into one shared epilogue fed by 24 register moves per row)
+    int dy = gy0;
+    while (dy < gy1) {
+      for (; dy < gy1; dy++) {  // A = X, B = Y
+        int ra, rb;
+        uint32_t c0, c1;
+        row_taps(dy, ra, rb, c0, c1);
+        if (ra != cx && ra == cy) break;  // down one source row: continue with A = Y
+        if (ra != cx) {
+          hrow(ra, HX);
+          cx = ra;
         }
-      } else {  // A = Y, B = X
-        if (ra != cy && ra == cx) {
-          par = false;
-          if (rb != cy) {
-            hrow(rb, HY);
-            cy = rb;
-          }
-        } else {
-          if (ra != cy) {
-            hrow(ra, HY);
-            cy = ra;
-          }
-          if (rb != cx) {
-            hrow(rb, HX);
-            cx = rb;
-          }
+        if (rb != cy) {
+          hrow(rb, HY);
+          cy = rb;
         }
-      }
-      if (par)
-        emit(dy, HY, HX, c0, c1);
-      else
         emit(dy, HX, HY, c0, c1);
+      }
+      for (; dy < gy1; dy++) {  // A = Y, B = X
+        int ra, rb;
+        uint32_t c0, c1;
+        row_taps(dy, ra, rb, c0, c1);
+        if (ra != cy && ra == cx) break;  // down one source row: continue with A = X
+        if (ra != cy) {
+          hrow(ra, HY);
+          cy = ra;
+        }
+        if (rb != cx) {
+          hrow(rb, HX);
+          cx = rb;
+        }
+        emit(dy, HY, HX, c0, c1);
+      }
     }
     return;
   }

@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 for v in $V; do
   lib=""; [ $v != new ] && lib="--lib build/ab/$v.so"
   d=gpurun_out/${TAG}_$v
+  echo "c5_parts: $v $(date +%T)" >> gpurun_out/${TAG}_progress.txt
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d $d -o run -- python3 bench.py $lib --config c5 --steps 40 --warmup 10 --unique 1024 --inflight 1 --no-cpu-baseline --no-host-check --parity-rows 0 --no-kernel-events > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
   python3 - "$d" "$v" <<'PY'
 import csv, glob, sys, collections

@@ -8,7 +8,8 @@ export TMPDIR=/tmp FFCV_K2_LOOP=0
 for v in $V; do
   lib=""; [ $v != new ] && lib="--lib build/ab/$v.so"
   d=gpurun_out/${TAG}_$v
-  timeout -s KILL 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d $d -o run -- python3 bench.py $lib --steps 48 --warmup 24 --uniform-launches --no-cpu-baseline --no-host-check --parity-rows 0 --no-kernel-events --no-later-epochs --no-c5 > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
+  echo "k2_parts: $v $(date +%T)" >> gpurun_out/${TAG}_progress.txt
+  timeout -s KILL 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d $d -o run -- python3 bench.py $lib --steps 24 --warmup 24 --uniform-launches --no-cpu-baseline --no-host-check --parity-rows 0 --no-kernel-events --no-later-epochs --no-c5 > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
   python3 - "$d" "$v" <<'PY'
 import csv, glob, sys, collections
 d, v = sys.argv[1], sys.argv[2]

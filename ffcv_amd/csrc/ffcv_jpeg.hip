@@ -103,6 +103,12 @@
 #define K2T 256  // K2 threads per workgroup
 #endif
 #define K2_COLS 128  // K2 fast path: output column-pair slots (out_w <= 256); K2T / K2_COLS row groups
+#ifndef K2_ROW_STAGE
+#define K2_ROW_STAGE 1  // per-band K2: plane tiles staged by rows (0: by dword index, rounds 1-4)
+#endif
+#ifndef K2_STAGE_ROWS
+#define K2_STAGE_ROWS 4  // rows a wave stages per batch of loads in flight
+#endif
 #ifndef K2_LDS
 #define K2_LDS 26624  // K2 dynamic LDS: the most that keeps 6 workgroups per CU (6 x 26 KB of 160 KB; 512 B granules); bigger bands take the general path (24 KB: 1% slower at C3, 32 KB: 3% slower)
 #endif
@@ -2520,6 +2526,46 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
       if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
       TPlane tp[3];
+#if K2_ROW_STAGE
+      // tile staging by rows: the tiles' rows, component after component, go
+      // to the waves round-robin (wave w stages rows w, w + 4, ...), lane l
+      // copies dword l (and l + 64) of a row; the row's source and LDS
+      // addresses are wave-uniform, so per row a lane spends a compare and an
+      // LDS address instead of a row / column division of its dword index;
+      // up to K2_STAGE_ROWS rows' loads are in flight before their LDS writes
+      {
+        const int wv = t >> 6, ln = t & 63;
+        const int n01 = trows[0] + trows[1], nrt = n01 + trows[2];
+        const int wmax = max(tpitch[0], max(tpitch[1], tpitch[2])) >> 2;
+        for (int cg = 0; cg < wmax; cg += 128)  // (one pass for tiles up to 512 bytes wide)
+        for (int g0 = wv; g0 < nrt; g0 += 4 * K2_STAGE_ROWS) {
+          uint32_t sv[K2_STAGE_ROWS][2];
+          int dst[K2_STAGE_ROWS], lim[K2_STAGE_ROWS];
+#pragma unroll
+          for (int q = 0; q < K2_STAGE_ROWS; q++) {
+            const int g = g0 + 4 * q;
+            const int c = g < trows[0] ? 0 : (g < n01 ? 1 : 2);
+            const int rr = g - (c == 0 ? 0 : (c == 1 ? trows[0] : n01));
+            const int pitch = c == 0 ? tpitch[0] : (c == 1 ? tpitch[1] : tpitch[2]);
+            lim[q] = g < nrt ? (pitch >> 2) - cg : 0;
+            const uint32_t *rp = (const uint32_t *)(gp[c].p + (uint64_t)((c == 0 ? ty0[0] : (c == 1 ? ty0[1] : ty0[2])) + rr) *
+                                                          (c == 0 ? gp[0].stride : (c == 1 ? gp[1].stride : gp[2].stride)) +
+                                                      (c == 0 ? tx0[0] : (c == 1 ? tx0[1] : tx0[2]))) + cg;
+            dst[q] = (((c == 0 ? toff[0] : (c == 1 ? toff[1] : toff[2])) + rr * pitch) >> 2) + cg;
+            sv[q][0] = ln < lim[q] ? rp[ln] : 0u;
+            sv[q][1] = ln + 64 < lim[q] ? rp[ln + 64] : 0u;
+          }
+#pragma unroll
+          for (int q = 0; q < K2_STAGE_ROWS; q++) {
+            uint32_t *tl = (uint32_t *)lds + dst[q];
+            if (ln < lim[q]) tl[ln] = sv[q][0];
+            if (ln + 64 < lim[q]) tl[ln + 64] = sv[q][1];
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) tp[c] = TPlane{(const uint8_t *)(lds + toff[c]), ty0[c], tx0[c], tpitch[c]};
+      }
+#else
       // tile staging: the first SU dwords per thread of every component are
       // loaded before any LDS write (one memory round trip, not one per
       // dword); row = i / wpr by a float reciprocal: exact while the +0.5
@@ -2554,6 +2600,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
         }
         tp[c] = TPlane{(const uint8_t *)tl, ty0[c], tx0[c], tpitch[c]};
       }
+#endif
       __syncthreads();
       K2_STOP_AT(2, a.out_stride != 77);  // diagnostics: + the plane tiles
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;

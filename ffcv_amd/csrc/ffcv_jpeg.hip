@@ -3201,6 +3201,29 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   // l of a wave writes dword l of the wave's 64-dword run), row of dword i
   // by a float reciprocal as in k2_band
   auto issue_tiles = [&](const K2Band &g) {
+#if K2_ROW_STAGE
+    // by rows, as k2_band: wave w copies rows w, w + 4, ... of the three
+    // tiles, lane l dword l (and l + 64, ...) of the row; the row's source
+    // and LDS addresses are wave-uniform
+    const int wv = t >> 6, ln = t & 63;
+    const int n01 = g.trows[0] + g.trows[1], nrt = n01 + g.trows[2];
+    for (int gr = wv; gr < nrt; gr += 4) {
+      const int c = gr < g.trows[0] ? 0 : (gr < n01 ? 1 : 2);
+      const int rr = gr - (c == 0 ? 0 : (c == 1 ? g.trows[0] : n01));
+      const int pitch = c == 0 ? g.tpitch[0] : (c == 1 ? g.tpitch[1] : g.tpitch[2]);
+      const uint8_t *src = (c == 0 ? plane[0] : (c == 1 ? plane[1] : plane[2])) +
+                           (uint64_t)((c == 0 ? g.ty0[0] : (c == 1 ? g.ty0[1] : g.ty0[2])) + rr) *
+                               (c == 0 ? pstride[0] : (c == 1 ? pstride[1] : pstride[2])) +
+                           (c == 0 ? g.tx0[0] : (c == 1 ? g.tx0[1] : g.tx0[2]));
+      uint8_t *dl = (uint8_t *)s_tile + (c == 0 ? g.toff[0] : (c == 1 ? g.toff[1] : g.toff[2])) + rr * pitch;
+      const int wpr = pitch >> 2;
+      for (int cg = 0; cg < wpr; cg += 64)
+        if (cg + ln < wpr)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 4 * (cg + ln)),
+                                           (__attribute__((address_space(3))) void *)(dl + 4 * cg), 4, 0, 0);
+    }
+    return;
+#endif
 #pragma unroll
     for (int c = 0; c < 3; c++) {
       const int wpr = max(g.tpitch[c] >> 2, 1), n = g.trows[c] * (g.tpitch[c] >> 2);

@@ -226,7 +226,9 @@ def parity_check(cfg, slots, order, batch, tile, offs, sizes, hs, ws, rows_total
     U = len(offs)
     rng = np.random.default_rng(seed)
     live = [sl for sl in slots if sl.get('last')]
-    per = max(64, rows_total // max(1, len(live)))
+    # rows_total < 0: every row of every slot's last launch (at the driver's
+    # 20 steps that is every timed row: each slot runs one timed launch)
+    per = (1 << 62) if rows_total < 0 else max(64, rows_total // max(1, len(live)))
     lut = O.normalize_lut(IMAGENET_MEAN, IMAGENET_STD) if norm else None
     decoder = 'libjpeg-turbo' if mode == 'jpg' and O.use_libjpeg_turbo() else ('oracle' if mode == 'jpg' else 'raw')
     checked = mism = crop_mism = 0
@@ -237,34 +239,41 @@ def parity_check(cfg, slots, order, batch, tile, offs, sizes, hs, ws, rows_total
             n = nb * batch
             edge = np.r_[np.arange(min(32, n)), np.arange(max(0, n - 32), n)]
             rest = np.setdiff1d(np.arange(n), edge)
-            pick = rng.choice(rest, size=min(rest.size, max(0, per - edge.size)), replace=False)
-            rows = np.unique(np.r_[edge, pick]).astype(np.int64)
-            ids = order[b0 * batch + rows].astype(np.uint64)
-            u = (ids % U).astype(np.int64)
-            d_rows = __import__('torch').from_numpy(rows).to(sl['out'].device)
-            got = sl['out'].index_select(0, d_rows).cpu().numpy()
-            got_crops = sl['crops'].index_select(0, d_rows).cpu().numpy()
-            crops, cyx = O.draw_batch(ids, hs[u], ws[u], 0, epoch, out_h=out, out_w=out, cutout_size=cut)
-            samples = [(tile[offs[i]:offs[i] + sizes[i]], int(hs[i]), int(ws[i]), 0 if mode == 'jpg' else 1)
-                       for i in u]
-            want = O.rrc_batch(samples, crops, out, out, cutout_yx=cyx, cutout_size=cut, fill=CUTOUT_FILL[cut],
-                               lut=lut, nthreads=cpu_threads())
-            if sl.get('cut') is not None and cut:
-                got_cut = sl['cut'].index_select(0, d_rows).cpu().numpy()
-                crop_mism += int((got_cut != cyx).any(1).sum())
-            crop_mism += int((got_crops != crops).any(1).sum())
-            bad = (got.view(np.uint8).reshape(len(rows), -1) != want.view(np.uint8).reshape(len(rows), -1)).any(1)
-            mism += int(bad.sum())
-            checked += len(rows)
-            launches.append({'rows_in_launch': n, 'checked': len(rows), 'mismatch': int(bad.sum()),
-                             'first_bad_rows': rows[bad][:4].tolist()})
+            pick = rest if per >= n else rng.choice(rest, size=min(rest.size, max(0, per - edge.size)), replace=False)
+            rows_all = np.unique(np.r_[edge, pick]).astype(np.int64)
+            bad_all = []
+            for c0 in range(0, len(rows_all), 1024):  # bounded host memory per chunk
+                rows = rows_all[c0:c0 + 1024]
+                ids = order[b0 * batch + rows].astype(np.uint64)
+                u = (ids % U).astype(np.int64)
+                d_rows = __import__('torch').from_numpy(rows).to(sl['out'].device)
+                got = sl['out'].index_select(0, d_rows).cpu().numpy()
+                got_crops = sl['crops'].index_select(0, d_rows).cpu().numpy()
+                crops, cyx = O.draw_batch(ids, hs[u], ws[u], 0, epoch, out_h=out, out_w=out, cutout_size=cut)
+                samples = [(tile[offs[i]:offs[i] + sizes[i]], int(hs[i]), int(ws[i]), 0 if mode == 'jpg' else 1)
+                           for i in u]
+                want = O.rrc_batch(samples, crops, out, out, cutout_yx=cyx, cutout_size=cut, fill=CUTOUT_FILL[cut],
+                                   lut=lut, nthreads=cpu_threads())
+                if sl.get('cut') is not None and cut:
+                    got_cut = sl['cut'].index_select(0, d_rows).cpu().numpy()
+                    crop_mism += int((got_cut != cyx).any(1).sum())
+                crop_mism += int((got_crops != crops).any(1).sum())
+                bad = (got.view(np.uint8).reshape(len(rows), -1) != want.view(np.uint8).reshape(len(rows), -1)).any(1)
+                bad_all.append(rows[bad])
+                mism += int(bad.sum())
+                checked += len(rows)
+            bad_rows = np.concatenate(bad_all) if bad_all else np.zeros(0, np.int64)
+            launches.append({'rows_in_launch': n, 'checked': len(rows_all), 'mismatch': int(bad_rows.size),
+                             'first_bad_rows': bad_rows[:4].tolist()})
     finally:
         if mode == 'jpg':
             O.use_libjpeg_turbo(False)
     return {'checked': checked, 'mismatch': mism, 'crop_mismatch': crop_mism, 'oracle_decoder': decoder,
             'launches': launches,
-            'note': 'rows of the timed launches still in each slot (every launch\'s first and last 32 + a seeded '
-                    'sample) vs the oracle under the same (seed, epoch, id) draws; bit-exact (fp16 bits) '
+            'rows_in_checked_launches': int(sum(l['rows_in_launch'] for l in launches)),
+            'note': ('every row of each slot\'s last launch' if rows_total < 0 else
+                     'rows of the timed launches still in each slot (every launch\'s first and last 32 + a seeded '
+                     'sample)') + ' vs the oracle under the same (seed, epoch, id) draws; bit-exact (fp16 bits) '
                     'required, checked after the timed region'}
 
 
@@ -280,7 +289,7 @@ def sub_result(config, timeout_s=240):
     import subprocess
     unique = {'c5': '1024', 'c2': '10000'}[config]
     cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', config, '--steps', '200', '--warmup', '20',
-           '--unique', unique, '--cpu-budget', '5', '--no-later-epochs', '--parity-rows', '512']
+           '--unique', unique, '--cpu-budget', '5', '--no-later-epochs', '--parity-rows', '-1']
     env = dict(os.environ)
     for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
         env.pop(k, None)
@@ -410,9 +419,10 @@ def main():
                     help='diagnostic A/B: raw path without the per-image plan / tap workspace (taps in every band)')
     ap.add_argument('--no-kernel-events', action='store_true',
                     help='do not record HIP events around each kernel of the timed launches (per-kernel roofline)')
-    ap.add_argument('--parity-rows', type=int, default=1536,
+    ap.add_argument('--parity-rows', type=int, default=-1,
                     help='rows of the timed launches compared bit for bit with the oracle after the timed region '
-                         '(0: skip)')
+                         '(-1: every row of each slot\'s last launch -- all timed rows at the driver\'s 20 steps; '
+                         '0: skip)')
     ap.add_argument('--entropy-index', action='store_true',
                     help='later-epoch rate: attach an entropy index, fill it with one untimed pass over '
                          'the timed samples (epoch 0), then time epoch 1 (new crops, no sync rounds)')
@@ -692,7 +702,7 @@ def main():
         per_rank = [float(x.item()) for x in allt]
         elapsed = max(per_rank)
     parity = None
-    if args.parity_rows > 0 and not args.only:
+    if args.parity_rows != 0 and not args.only:
         parity = parity_check(args.config, slots, order, batch, tile, offs, sizes, hs, ws, args.parity_rows)
         if dist:
             t = torch.tensor([parity['checked'], parity['mismatch'], parity['crop_mismatch']], dtype=torch.int64,

@@ -16,6 +16,9 @@ typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));  // v_dot2_u
 // reference's libffcv.cpp:33-42 signature) runs the very same functions on
 // the CPU.  These helpers pick the gfx950 instruction on the device pass.
 #define FFCV_HD __host__ __device__ __forceinline__
+// raw buffer resources: a load past num_records returns 0, a store is dropped
+#define BUF_OOR 0x7ffffff0u  // an offset past every buffer's num_records
+#define BUF_CFG 0x00020000   // raw buffer resource word 3 (gfx9 family)
 
 FFCV_HD int ffcv_f2i_rn(float x) {  // round half to even, like cvRound
 #if defined(__HIP_DEVICE_COMPILE__)

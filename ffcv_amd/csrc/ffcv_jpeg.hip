@@ -103,12 +103,6 @@
 #define K2T 256  // K2 threads per workgroup
 #endif
 #define K2_COLS 128  // K2 fast path: output column-pair slots (out_w <= 256); K2T / K2_COLS row groups
-#ifndef K2_ROW_STAGE
-#define K2_ROW_STAGE 1  // per-band K2: plane tiles staged by rows (0: by dword index, rounds 1-4)
-#endif
-#ifndef K2_STAGE_ROWS
-#define K2_STAGE_ROWS 4  // rows a wave stages per batch of loads in flight
-#endif
 #ifndef K2_LDS
 #define K2_LDS 26624  // K2 dynamic LDS: the most that keeps 6 workgroups per CU (6 x 26 KB of 160 KB; 512 B granules); bigger bands take the general path (24 KB: 1% slower at C3, 32 KB: 3% slower)
 #endif
@@ -390,8 +384,7 @@ FFCV_DEV uint32_t make_pair(const TB &T, int slot, int bits, const uint32_t *L, 
 // these static counts the next step waits for its load with vmcnt(3) instead
 // of draining the previous steps' coefficient stores (vmcnt(0), which the
 // conditional global stores forced).
-#define BUF_OOR 0x7ffffff0u  // an offset past every buffer's num_records
-#define BUF_CFG 0x00020000   // raw buffer resource word 3 (gfx9 family)
+// (BUF_OOR / BUF_CFG: device_common.h)
 struct BufReader {
   __amdgpu_buffer_rsrc_t rs;
   uint64_t acc;
@@ -2526,46 +2519,6 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
       if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
       TPlane tp[3];
-#if K2_ROW_STAGE
-      // tile staging by rows: the tiles' rows, component after component, go
-      // to the waves round-robin (wave w stages rows w, w + 4, ...), lane l
-      // copies dword l (and l + 64) of a row; the row's source and LDS
-      // addresses are wave-uniform, so per row a lane spends a compare and an
-      // LDS address instead of a row / column division of its dword index;
-      // up to K2_STAGE_ROWS rows' loads are in flight before their LDS writes
-      {
-        const int wv = t >> 6, ln = t & 63;
-        const int n01 = trows[0] + trows[1], nrt = n01 + trows[2];
-        const int wmax = max(tpitch[0], max(tpitch[1], tpitch[2])) >> 2;
-        for (int cg = 0; cg < wmax; cg += 128)  // (one pass for tiles up to 512 bytes wide)
-        for (int g0 = wv; g0 < nrt; g0 += 4 * K2_STAGE_ROWS) {
-          uint32_t sv[K2_STAGE_ROWS][2];
-          int dst[K2_STAGE_ROWS], lim[K2_STAGE_ROWS];
-#pragma unroll
-          for (int q = 0; q < K2_STAGE_ROWS; q++) {
-            const int g = g0 + 4 * q;
-            const int c = g < trows[0] ? 0 : (g < n01 ? 1 : 2);
-            const int rr = g - (c == 0 ? 0 : (c == 1 ? trows[0] : n01));
-            const int pitch = c == 0 ? tpitch[0] : (c == 1 ? tpitch[1] : tpitch[2]);
-            lim[q] = g < nrt ? (pitch >> 2) - cg : 0;
-            const uint32_t *rp = (const uint32_t *)(gp[c].p + (uint64_t)((c == 0 ? ty0[0] : (c == 1 ? ty0[1] : ty0[2])) + rr) *
-                                                          (c == 0 ? gp[0].stride : (c == 1 ? gp[1].stride : gp[2].stride)) +
-                                                      (c == 0 ? tx0[0] : (c == 1 ? tx0[1] : tx0[2]))) + cg;
-            dst[q] = (((c == 0 ? toff[0] : (c == 1 ? toff[1] : toff[2])) + rr * pitch) >> 2) + cg;
-            sv[q][0] = ln < lim[q] ? rp[ln] : 0u;
-            sv[q][1] = ln + 64 < lim[q] ? rp[ln + 64] : 0u;
-          }
-#pragma unroll
-          for (int q = 0; q < K2_STAGE_ROWS; q++) {
-            uint32_t *tl = (uint32_t *)lds + dst[q];
-            if (ln < lim[q]) tl[ln] = sv[q][0];
-            if (ln + 64 < lim[q]) tl[ln + 64] = sv[q][1];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 3; c++) tp[c] = TPlane{(const uint8_t *)(lds + toff[c]), ty0[c], tx0[c], tpitch[c]};
-      }
-#else
       // tile staging: the first SU dwords per thread of every component are
       // loaded before any LDS write (one memory round trip, not one per
       // dword); row = i / wpr by a float reciprocal: exact while the +0.5
@@ -2600,7 +2553,6 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
         }
         tp[c] = TPlane{(const uint8_t *)tl, ty0[c], tx0[c], tpitch[c]};
       }
-#endif
       __syncthreads();
       K2_STOP_AT(2, a.out_stride != 77);  // diagnostics: + the plane tiles
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
@@ -3201,29 +3153,6 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   // l of a wave writes dword l of the wave's 64-dword run), row of dword i
   // by a float reciprocal as in k2_band
   auto issue_tiles = [&](const K2Band &g) {
-#if K2_ROW_STAGE
-    // by rows, as k2_band: wave w copies rows w, w + 4, ... of the three
-    // tiles, lane l dword l (and l + 64, ...) of the row; the row's source
-    // and LDS addresses are wave-uniform
-    const int wv = t >> 6, ln = t & 63;
-    const int n01 = g.trows[0] + g.trows[1], nrt = n01 + g.trows[2];
-    for (int gr = wv; gr < nrt; gr += 4) {
-      const int c = gr < g.trows[0] ? 0 : (gr < n01 ? 1 : 2);
-      const int rr = gr - (c == 0 ? 0 : (c == 1 ? g.trows[0] : n01));
-      const int pitch = c == 0 ? g.tpitch[0] : (c == 1 ? g.tpitch[1] : g.tpitch[2]);
-      const uint8_t *src = (c == 0 ? plane[0] : (c == 1 ? plane[1] : plane[2])) +
-                           (uint64_t)((c == 0 ? g.ty0[0] : (c == 1 ? g.ty0[1] : g.ty0[2])) + rr) *
-                               (c == 0 ? pstride[0] : (c == 1 ? pstride[1] : pstride[2])) +
-                           (c == 0 ? g.tx0[0] : (c == 1 ? g.tx0[1] : g.tx0[2]));
-      uint8_t *dl = (uint8_t *)s_tile + (c == 0 ? g.toff[0] : (c == 1 ? g.toff[1] : g.toff[2])) + rr * pitch;
-      const int wpr = pitch >> 2;
-      for (int cg = 0; cg < wpr; cg += 64)
-        if (cg + ln < wpr)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 4 * (cg + ln)),
-                                           (__attribute__((address_space(3))) void *)(dl + 4 * cg), 4, 0, 0);
-    }
-    return;
-#endif
 #pragma unroll
     for (int c = 0; c < 3; c++) {
       const int wpr = max(g.tpitch[c] >> 2, 1), n = g.trows[c] * (g.tpitch[c] >> 2);

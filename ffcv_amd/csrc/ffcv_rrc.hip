@@ -158,10 +158,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     // l + 64: the row address and its chunk count are wave-uniform (scalar),
     // a lane's chunk offset is fixed, and a wave has up to RRC_STAGE_ROWS
     // rows' loads in flight before its LDS writes
-    // (readfirstlane: the compiler does not know t >> 6 is wave-uniform).
-    // Each row is read through a raw buffer resource of exactly its chunks:
-    // lanes past the row's end read zeros without a branch
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+    const int wv = t >> 6, ln = t & 63;
     for (int cg = 0; cg < nch; cg += 128)  // (one pass for rows up to 2 KB: crops up to 677 px wide)
       for (int rb0 = wv; rb0 < nrows; rb0 += 4 * RRC_STAGE_ROWS) {
         uint4 v[RRC_STAGE_ROWS][2];
@@ -170,16 +167,16 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
           const int r = rb0 + 4 * q;
           const uint64_t ra = row0 + (uint64_t)r * src.step;
           // chunks holding bytes of this row (none past the dataset's end)
-          const int lim = r < nrows ? min(max((int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg, 0), 128) : 0;
-          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-              (void *)(uintptr_t)((ra & ~(uint64_t)15) + 16 * (uint64_t)cg), 0, 16 * lim, BUF_CFG);
-          v[q][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * ln, 0, 0));
-          v[q][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * ln + 1024, 0, 0));
+          const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
+          const uint4 *rp = (const uint4 *)(uintptr_t)(ra & ~(uint64_t)15) + cg;
+          v[q][0] = ln < lim ? rp[ln] : make_uint4(0, 0, 0, 0);
+          v[q][1] = ln + 64 < lim ? rp[ln + 64] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < RRC_STAGE_ROWS; q++) {
           const int r = rb0 + 4 * q;
-          const int lim = r < nrows ? min(nch - cg, 128) : 0;
+          const uint64_t ra = row0 + (uint64_t)r * src.step;
+          const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
           if (ln < lim) s_src[r * nch + cg + ln] = v[q][0];
           if (ln + 64 < lim) s_src[r * nch + cg + ln + 64] = v[q][1];
         }

@@ -482,6 +482,15 @@ def main():
         tile, offs, sizes, hs, ws = make_unique(mode, side, args.unique, 0, workers)
     U = len(offs)
     tile_len = int(offs[-1] + (sizes[-1] + 7) // 8 * 8)
+    # Huffman symbols per image (DC + AC incl. EOB / ZRL) over an even sample
+    # of the unique encodings, by the CPU decoder's Huffman loop: K1's
+    # lane-instructions per decoded symbol in the roofline
+    scan = None
+    if mode == 'jpg' and rank == 0:
+        pick = np.unique(np.linspace(0, U - 1, min(U, 2048)).astype(np.int64))
+        st = L.jpeg_scan_stats([tile[int(offs[i]):int(offs[i]) + int(sizes[i])] for i in pick])
+        scan = {'symbols_per_image': float(st[:, 0].mean()), 'blocks_per_image': float(st[:, 1].mean()),
+                'scan_bytes_per_image': float(st[:, 2].mean()), 'sampled_encodings': int(len(pick))}
     reps = (N + U - 1) // U
 
     # ---- HBM-resident dataset: U encodings replicated at distinct addresses
@@ -944,6 +953,15 @@ def main():
                     e['cycles_per_wave'] = round(cyc, 0)
                     e['us_per_wave_at_2.4GHz'] = round(cyc / 2400.0, 2)
                     e['waves_per_image'] = round(q['SQ_WAVES'] / q['images'], 2)
+                if scan and n.startswith('jpeg_entropy_kernel'):
+                    # lane-instructions (64 per wave instruction) per decoded Huffman symbol
+                    e['symbols_per_image'] = round(scan['symbols_per_image'], 1)
+                    e['valu_lane_instr_per_symbol'] = round(64 * q['valu_per_image'] / scan['symbols_per_image'], 1)
+                    if q.get('salu_per_image'):
+                        e['salu_per_symbol'] = round(q['salu_per_image'] / scan['symbols_per_image'], 3)
+                    e['symbols_note'] = (f"mean over {scan['sampled_encodings']} of the unique encodings "
+                                         f"(ffcv_jpeg_scan_stats; {scan['blocks_per_image']:.0f} blocks, "
+                                         f"{scan['scan_bytes_per_image']:.0f} entropy-coded bytes per image)")
                 if pm and n in pm and 'fetch_size_kb' in pm[n]:
                     b = (pm[n]['fetch_size_kb'] + pm[n]['write_size_kb']) * 1024.0 / pm[n]['images']
                     e['hbm_bytes_per_image_counter'] = round(b, 1)

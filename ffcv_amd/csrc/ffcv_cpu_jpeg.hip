@@ -439,8 +439,9 @@ void plane_setup(Dec &d, Scratch &S, int stride[3], int16_t qm[3][64]) {
 
 // Huffman decode of the whole scan: emit(component, block x, block y,
 // coefficients in natural order with the absolute DC) for every coded block.
+// nsym (optional): incremented by the Huffman symbols (DC and AC) decoded.
 template <class Emit>
-void decode_scan(const uint8_t *b, const Dec &d, Emit &&emit) {
+void decode_scan(const uint8_t *b, const Dec &d, Emit &&emit, uint64_t *nsym = nullptr) {
   const int mcux = (d.W + 8 * d.hmax - 1) / (8 * d.hmax), mcuy = (d.H + 8 * d.vmax - 1) / (8 * d.vmax);
   Bits br{b + d.ecs, b + d.ecs_end};
   int pred[3] = {0, 0, 0};
@@ -474,17 +475,22 @@ void decode_scan(const uint8_t *b, const Dec &d, Emit &&emit) {
           if (s) s = extend(br.get(s), s);
           pred[ci] += s;
           blk[0] = (int16_t)pred[ci];
-          for (int z = 1; z < 64; z++) {
+          uint64_t ns = 1;
+          for (int z = 1; z < 64; z++, ns++) {
             const int rs = decode_sym(br, ha), r = rs >> 4;
             s = rs & 15;
             if (s) {
               z += r;
               blk[kNatural[z]] = (int16_t)extend(br.get(s), s);
             } else {
-              if (r != 15) break;
+              if (r != 15) {
+                ns++;  // (the EOB that ends the loop)
+                break;
+              }
               z += 15;
             }
           }
+          if (nsym) *nsym += ns;
           emit(ci, bx, by, blk);
         }
     }
@@ -1054,6 +1060,33 @@ int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes, con
   for (auto &x : th) x.join();
   if (err_k < batch) ffcv::set_error("sample %d: %s", err_k, err_msg.c_str());
   return FFCV_OK;
+}
+
+// Measurement helper (bench.py's K1 lane-instructions per symbol): per
+// image, the Huffman symbols (DC + AC, EOB and ZRL included) and the blocks of
+// its scan.  stats[3k..3k+2] = symbols, blocks, entropy-coded bytes; an image
+// that does not parse gets zeros and -1 is returned after the rest.
+int ffcv_jpeg_scan_stats(const uint8_t *const *data, const uint64_t *sizes, int n, uint64_t *stats) {
+  if ((!data || !sizes || !stats) && n > 0) {
+    ffcv::set_error("ffcv_jpeg_scan_stats: invalid arguments");
+    return FFCV_EINVAL;
+  }
+  int rc = FFCV_OK;
+  for (int k = 0; k < n; k++) {
+    uint64_t *o = stats + 3 * (size_t)k;
+    o[0] = o[1] = o[2] = 0;
+    Dec d;
+    if (!data[k] || parse(data[k], sizes[k], d)) {
+      rc = -1;
+      continue;
+    }
+    uint64_t nsym = 0, nblk = 0;
+    decode_scan(data[k], d, [&](int, int, int, const int16_t *) { nblk++; }, &nsym);
+    o[0] = nsym;
+    o[1] = nblk;
+    o[2] = d.ecs_end - d.ecs;
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -93,6 +93,7 @@ _SIGS = {
     'ffcv_rrc_raw_workspace_bytes': (c_uint64, [c_int, c_int, c_int]),
     'ffcv_gather_samples': (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_int, c_void_p]),
     'ffcv_gather_raw_batch': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_uint64]),
+    'ffcv_jpeg_scan_stats': (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     'ffcv_jpeg_create': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64]),
     'ffcv_jpeg_destroy': (c_int, [c_void_p]),
     'ffcv_jpeg_create_arena': (c_int, [c_void_p, c_int, c_uint32, c_uint32, c_uint64, c_uint64]),
@@ -246,6 +247,21 @@ def _imdecode(fn, source, dst, source_height, source_width, crop_height, crop_wi
     return fn(source.ctypes.data, source.size, int(source_height), int(source_width),
               dst.ctypes.data, int(crop_height), int(crop_width), int(offset_x), int(offset_y),
               int(scale_factor_num), int(scale_factor_denom), bool(enable_crop), bool(do_flip))
+
+
+def jpeg_scan_stats(images):
+    """(symbols, blocks, entropy-coded bytes) per JPEG, uint64 (n, 3), from the
+    CPU decoder's Huffman loop (ffcv_jpeg_scan_stats); rows of images that
+    do not parse are zero."""
+    images = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+    n = len(images)
+    ptrs = np.array([im.ctypes.data for im in images], dtype=np.uint64)
+    sizes = np.array([im.size for im in images], dtype=np.uint64)
+    stats = np.zeros((max(n, 1), 3), dtype=np.uint64)
+    rc = lib().ffcv_jpeg_scan_stats(ptrs.ctypes.data, sizes.ctypes.data, n, stats.ctypes.data)
+    if rc not in (0, -1):
+        raise RuntimeError('ffcv_jpeg_scan_stats: ' + lib().ffcv_last_error().decode(errors='replace'))
+    return stats[:n]
 
 
 def cpu_decode_batch(images, heights, widths, modes, out: np.ndarray, crops=None, nthreads=1):

@@ -167,6 +167,14 @@ int ffcv_cpu_decode_batch(const uint8_t *const *data, const uint64_t *sizes,
                           int out_h, int out_w, uint8_t *out, uint64_t out_stride,
                           int nthreads, int32_t *status);
 
+/* Measurement helper (new; no reference counterpart): per image k of n,
+ * stats[3k] = Huffman symbols of its scan (DC + AC, EOB / ZRL included),
+ * stats[3k+1] = blocks, stats[3k+2] = entropy-coded bytes (host decode by the
+ * CPU decoder's Huffman loop).  bench.py's K1 lane-instructions per symbol.
+ * Returns FFCV_OK, -1 when an image does not parse (its stats are 0), or
+ * FFCV_EINVAL. */
+int ffcv_jpeg_scan_stats(const uint8_t *const *data, const uint64_t *sizes, int n, uint64_t *stats);
+
 /* imdecode's signature and semantics, executed by the gfx950 JPEG kernels
  * (per-thread stream and decoder context; host buffers in and out). */
 int ffcv_imdecode_device(unsigned char *input_buffer, uint64_t input_size,

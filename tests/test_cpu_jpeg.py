@@ -253,3 +253,21 @@ def test_cpu_decode_batch(hip_lib, oracle):
     st = L.cpu_decode_batch(short, hs, ws, modes, full, nthreads=3)
     assert st[5] == -1 and (np.delete(st, 5) == 0).all()
     assert b'raw sample 5' in L.lib().ffcv_last_error()
+
+
+def test_jpeg_scan_stats(hip_lib):
+    """ffcv_jpeg_scan_stats (bench.py's K1 symbols per image): a constant
+    image codes every block as DC + EOB, so symbols == 2 x blocks exactly;
+    the block count follows the MCU grid; a natural image has more symbols
+    than a constant one of the same size; junk reports zeros and -1."""
+    from ffcv_amd import libffcv as L
+    flat = np.full((48, 40, 3), 117, np.uint8)
+    nat = natural_image(np.random.default_rng(3), 48, 40)
+    blobs = [encode_jpeg(flat, 90, '4:2:0'), encode_jpeg(flat, 90, '4:4:4'), encode_jpeg(nat, 90, '4:2:0')]
+    st = L.jpeg_scan_stats([np.frombuffer(b, np.uint8) for b in blobs])
+    # 4:2:0: 48 x 40 -> 3 x 3 MCUs (16 x 16) of 4 Y + Cb + Cr; 4:4:4: 6 x 5 MCUs of 3 blocks
+    assert st[0, 1] == 3 * 3 * 6 and st[1, 1] == 6 * 5 * 3 and st[2, 1] == st[0, 1]
+    assert st[0, 0] == 2 * st[0, 1] and st[1, 0] == 2 * st[1, 1]
+    assert st[2, 0] > st[0, 0] and 0 < st[0, 2] < len(blobs[0])
+    bad = L.jpeg_scan_stats([np.zeros(64, np.uint8)])
+    assert bad.tolist() == [[0, 0, 0]]

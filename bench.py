@@ -409,6 +409,8 @@ def main():
                     help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 1 IDCT, bit 2 K2)')
     ap.add_argument('--split', default='',
                     help='diagnostic: batches per timed launch, comma-separated (must sum to --steps)')
+    ap.add_argument('--draw-scale', default='',
+                    help='diagnostic: RRC scale range lo,hi with ratio 1 (use with --parity-rows 0)')
     ap.add_argument('--uniform-launches', action='store_true',
                     help='profiling: ceil(K/G) launches of near-equal size (no half-size first launch)')
     ap.add_argument('--no-later-epochs', action='store_true',
@@ -558,6 +560,9 @@ def main():
     dp.cutout_size = cut
     dp.scale[0], dp.scale[1] = 0.08, 1.0
     dp.ratio[0], dp.ratio[1] = 0.75, 4 / 3
+    if args.draw_scale:  # diagnostic (timing by crop size; the parity oracle assumes the defaults)
+        dp.scale[0], dp.scale[1] = (float(x) for x in args.draw_scale.split(','))
+        dp.ratio[0] = dp.ratio[1] = 1.0
     dp.loader_seed = 0
     dp.epoch = 0
     eidx = None

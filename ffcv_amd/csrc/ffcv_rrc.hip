@@ -195,118 +195,6 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
   const int nq = out_w >> 2;  // column quads
   if (staged && (out_w & 3) == 0 && nq <= RRC_THREADS && aligned4 &&
       ((P.kind == 3 && P.vec_end == 3 * out_w) || P.kind == 2)) {
-    if (P.kind == 2 && P.scale_x < 2.0 && P.scale_y < 2.0 && (out_w >> 1) <= RRC_THREADS) {
-      // ResizeArea_Invoker for scales in [1, 2): every destination index takes
-      // at most 3 consecutive source indices, so a fixed 3-tap body with zero
-      // weights past `hi` is exact (x + S * 0.f == x for the non-negative
-      // sums here, and an index past hi reads a clamped, staged pixel).  The
-      // horizontal sums of a source row (buf in the reference) do not depend
-      // on the destination row, so the walk keeps the last three rows' sums
-      // and computes ~scale_y new rows per destination row.  Two columns per
-      // thread (one row group walks the band): few registers.
-      const int nq2 = out_w >> 1;
-      const int q2 = t;
-      if (q2 >= nq2) return;
-      const int dc0 = 2 * q2;
-      AreaTaps tx[2];
-      int xb[2];
-      float wx[2][3];
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        tx[j] = area_taps(P.sw, P.scale_x, ep.src_x(dc0 + j));
-        xb[j] = tx[j].lo;
-#pragma unroll
-        for (int k = 0; k < 3; k++) wx[j][k] = tx[j].lo + k <= tx[j].hi ? tx[j].w(tx[j].lo + k) : 0.f;
-      }
-      uint32_t cm = 0;
-#pragma unroll
-      for (int j = 0; j < 2; j++) cm |= ep.in_cut(ep.cut_y, dc0 + j) ? 1u << j : 0u;
-      auto hsum = [&](int r, float B[6]) {  // buf of source row r for both columns, table order
-        const uint8_t *row = L.row(r);
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-#pragma unroll
-          for (int c = 0; c < 3; c++) {
-            float b = 0.f;
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-              const int sx = min(xb[j] + k, tx[j].hi);
-              b = b + (float)row[sx * 3 + c] * wx[j][k];
-            }
-            B[3 * j + c] = b;
-          }
-        }
-      };
-      int R[3] = {-1, -1, -1};
-      float BR[3][6];
-      for (int dy = oy0; dy < oy1; dy++) {
-        const AreaTaps ty = s_at[dy - oy0];
-        float NB[3][6];
-        int NR[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          const int r = min(ty.lo + k, ty.hi);  // uniform: every thread walks the same rows
-          NR[k] = r;
-          if (r == R[0]) {
-#pragma unroll
-            for (int i = 0; i < 6; i++) NB[k][i] = BR[0][i];
-          } else if (r == R[1]) {
-#pragma unroll
-            for (int i = 0; i < 6; i++) NB[k][i] = BR[1][i];
-          } else if (r == R[2]) {
-#pragma unroll
-            for (int i = 0; i < 6; i++) NB[k][i] = BR[2][i];
-          } else if (k > 0 && r == NR[k - 1]) {
-#pragma unroll
-            for (int i = 0; i < 6; i++) NB[k][i] = NB[k - 1][i];
-          } else {
-            hsum(r, NB[k]);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          R[k] = NR[k];
-#pragma unroll
-          for (int i = 0; i < 6; i++) BR[k][i] = NB[k][i];
-        }
-        float bt[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) bt[k] = ty.lo + k <= ty.hi ? ty.w(ty.lo + k) : 0.f;
-        int v[6];
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-          float sum = bt[0] * NB[0][i];
-          sum = sum + bt[1] * NB[1][i];
-          sum = sum + bt[2] * NB[2][i];
-          v[i] = sat_u8i(ffcv_f2i_rn(sum));
-        }
-        if (cm && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
-#pragma unroll
-          for (int j = 0; j < 2; j++)
-            if ((cm >> j) & 1) {
-              v[3 * j] = ep.fill[0];
-              v[3 * j + 1] = ep.fill[1];
-              v[3 * j + 2] = ep.fill[2];
-            }
-        }
-        const uint64_t px = (uint64_t)dy * out_w + dc0;
-        if (FP16) {  // 12 bytes, 4-byte aligned
-          uint32_t h[6];
-#pragma unroll
-          for (int i = 0; i < 6; i++) h[i] = s_lut[v[i] * 3 + i % 3];
-          uint32_t *o32 = (uint32_t *)((uint16_t *)o + px * 3);
-          o32[0] = h[0] | (h[1] << 16);
-          o32[1] = h[2] | (h[3] << 16);
-          o32[2] = h[4] | (h[5] << 16);
-        } else {  // 6 bytes, 2-byte aligned
-          uint16_t *o16 = (uint16_t *)((uint8_t *)o + px * 3);
-          __builtin_nontemporal_store((uint16_t)(v[0] | (v[1] << 8)), o16);
-          __builtin_nontemporal_store((uint16_t)(v[2] | (v[3] << 8)), o16 + 1);
-          __builtin_nontemporal_store((uint16_t)(v[4] | (v[5] << 8)), o16 + 2);
-        }
-      }
-      return;
-    }
     // row groups: tpg threads (a power of two >= nq, >= 64) per group, each
     // group walks its own slice of the band's rows
     int tpg = 64;
@@ -360,6 +248,95 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
       AreaTaps tx[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) tx[j] = area_taps(P.sw, P.scale_x, ep.src_x(dx0 + j));
+      RRC_STOP_AT(4, p.cutout_fill[3] != 77);  // diagnostics: + the area walk's column taps
+      if (P.scale_x < 2.0 && P.scale_y < 2.0) {
+        // Scales in [1, 2): a destination index takes at most 3 consecutive
+        // source indices, so a fixed 3-tap horizontal body with zero weights
+        // past `hi` is exact (x + S * 0.f == x for the non-negative sums
+        // here).  buf of a source row (the horizontal sums)
+        // does not depend on the destination row: each destination row dy
+        // sums its source rows lo..hi in ascending order (sum = w(lo) * B(lo),
+        // then sum += w(r) * B(r): the reference's order), and consecutive
+        // rows share at most their boundary source row, so one cached row of
+        // sums (Hc, source row cr) covers the reuse (any other reuse
+        // recomputes, exactly).  The rows are wave-uniform (a row group is
+        // whole waves): the loop bounds and the cache test are scalar.
+        int xo[4];  // the first tap pixel's byte offset in a row
+        float wx[4][3];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          xo[j] = 3 * tx[j].lo;
+#pragma unroll
+          for (int k = 0; k < 3; k++) wx[j][k] = tx[j].lo + k <= tx[j].hi ? tx[j].w(tx[j].lo + k) : 0.f;
+        }
+        // A column's three tap pixels lo, lo + 1, lo + 2 are 9 consecutive
+        // bytes: three ALIGNED 4-byte LDS reads cover them at any alignment
+        // and v_alignbyte shifts them into place (bytes at fixed positions,
+        // converted by v_cvt_f32_ubyte0-3).  Misaligned LDS reads (the 2- and
+        // 4-byte reads the compiler forms from adjacent byte reads) made this
+        // walk ~5x slower per pixel than the linear one.  A tap past hi has
+        // weight 0 and reads a byte of the staged rows or the LDS that
+        // follows them (finite: 0 * x == 0).
+        auto hsum = [&](int r, float B[12]) {
+          const uint8_t *row = L.row(r);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint8_t *q = row + xo[j];
+            const uint32_t *qa = (const uint32_t *)__builtin_align_down(q, 4);
+            const uint32_t sh = (uint32_t)(q - (const uint8_t *)qa);  // 0..3
+            const uint32_t d0 = qa[0], d1 = qa[1], d2 = qa[2];
+            uint32_t e[3];
+            e[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            e[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            e[2] = d2 >> (8 * sh);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+              float b = 0.f;
+#pragma unroll
+              for (int k = 0; k < 3; k++) {
+                const int i = 3 * k + c;
+                b = b + (float)((e[i >> 2] >> (8 * (i & 3))) & 0xffu) * wx[j][k];
+              }
+              B[3 * j + c] = b;
+            }
+          }
+        };
+        int cr = -1;
+        float Hc[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) Hc[i] = 0.f;
+        for (int dy = gy0; dy < gy1; dy++) {
+          const AreaTaps ty = s_at[dy - oy0];
+          float S[12];
+          for (int r = ty.lo; r <= ty.hi; r++) {
+            float H[12];
+            if (r == cr) {
+#pragma unroll
+              for (int i = 0; i < 12; i++) H[i] = Hc[i];
+            } else {
+              hsum(r, H);
+            }
+            const float w = ty.w(r);
+            if (r == ty.lo) {
+#pragma unroll
+              for (int i = 0; i < 12; i++) S[i] = w * H[i];
+            } else {
+#pragma unroll
+              for (int i = 0; i < 12; i++) S[i] = S[i] + w * H[i];
+            }
+            if (r == ty.hi) {
+#pragma unroll
+              for (int i = 0; i < 12; i++) Hc[i] = H[i];
+              cr = r;
+            }
+          }
+          int v[12];
+#pragma unroll
+          for (int i = 0; i < 12; i++) v[i] = sat_u8i(ffcv_f2i_rn(S[i]));
+          put(dy, v);
+        }
+        return;
+      }
       for (int dy = gy0; dy < gy1; dy++) {
         const AreaTaps ty = s_at[dy - oy0];
         int v[12];

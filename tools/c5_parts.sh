@@ -1,16 +1,21 @@
 #!/bin/bash
 # C5 (raw RRC 448) instruction / time split by diagnostic stop builds
-# (-DRRC_STOP=n: 1 set-up only, 2 + staging, 3 + the walk's column taps):
+# (-DRRC_STOP=n: 1 set-up only, 2 + staging, 3 + the linear walk's column taps,
+# 4 + the area walk's column taps):
 #   tools/c5_parts.sh <tag> "new rrcstop1 rrcstop2 rrcstop3"
 # one rocprofv3 SQ pass (+ kernel trace for durations) per build, launches of
 # 2,560 images one at a time; prints VALU / SALU / LDS per image and ns per image.
+# EXTRA: more bench.py arguments (e.g. EXTRA="--draw-scale 0.79,0.9").
 TAG=$1; V=${2:-"new rrcstop1 rrcstop2 rrcstop3"}
 export TMPDIR=/tmp
+# warm the box first (first import of torch, the /tmp sample cache) with
+# output going to a file: a profiled run that is silent for 3 minutes is killed
+timeout -k 10 300 python3 bench.py --config c5 --steps 2 --warmup 1 --unique 1024 --no-cpu-baseline --parity-rows 0 --no-kernel-events > gpurun_out/${TAG}_warm.log 2>&1 || { tail -3 gpurun_out/${TAG}_warm.log; exit 1; }
 for v in $V; do
   lib=""; [ $v != new ] && lib="--lib build/ab/$v.so"
   d=gpurun_out/${TAG}_$v
   echo "c5_parts: $v $(date +%T)" >> gpurun_out/${TAG}_progress.txt
-  timeout -s KILL 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d $d -o run -- python3 bench.py $lib --config c5 --steps 40 --warmup 10 --unique 1024 --inflight 1 --no-cpu-baseline --no-host-check --parity-rows 0 --no-kernel-events > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d $d -o run -- python3 bench.py $lib --config c5 --steps 40 --warmup 10 --unique 1024 --inflight 1 --no-cpu-baseline --no-host-check --parity-rows 0 --no-kernel-events $EXTRA > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
   python3 - "$d" "$v" <<'PY'
 import csv, glob, sys, collections
 d, v = sys.argv[1], sys.argv[2]

@@ -16,8 +16,8 @@ descriptor gather, crop/cutout draws, parse, de-stuff, parallel Huffman
 decode of the crop's coefficients), jpeg_idct_kernel (K1b: DC prediction,
 dequantise + ifast IDCT of the crop's blocks) and jpeg_color_resize_kernel
 (K2: upsample + colour, INTER_AREA, cutout, LUT; one workgroup per 16-row
-band, or jpeg_rrc_loop_kernel, seven bands per workgroup, for launches of
->= 8,192 images).  The 1.28M-entry dataset
+band; the band-loop jpeg_rrc_loop_kernel only with FFCV_K2_LOOP=1).  The
+1.28M-entry dataset
 is built from U unique encodings replicated at distinct HBM addresses.
 
 After the timed region (outside it) the rows each slot's last timed launch
@@ -409,6 +409,8 @@ def main():
                     help='diagnostic: timed launches run only these decode kernels (bit 0 K1, bit 1 IDCT, bit 2 K2)')
     ap.add_argument('--split', default='',
                     help='diagnostic: batches per timed launch, comma-separated (must sum to --steps)')
+    ap.add_argument('--draw-ratio', default='',
+                    help='diagnostic: RRC aspect-ratio range lo,hi (after --draw-scale; use with --parity-rows 0)')
     ap.add_argument('--draw-scale', default='',
                     help='diagnostic: RRC scale range lo,hi with ratio 1 (use with --parity-rows 0)')
     ap.add_argument('--uniform-launches', action='store_true',
@@ -563,6 +565,8 @@ def main():
     if args.draw_scale:  # diagnostic (timing by crop size; the parity oracle assumes the defaults)
         dp.scale[0], dp.scale[1] = (float(x) for x in args.draw_scale.split(','))
         dp.ratio[0] = dp.ratio[1] = 1.0
+    if args.draw_ratio:
+        dp.ratio[0], dp.ratio[1] = (float(x) for x in args.draw_ratio.split(','))
     dp.loader_seed = 0
     dp.epoch = 0
     eidx = None
@@ -836,12 +840,10 @@ def main():
     hbm = {'bound': 'hbm', 'achieved': round(hbm_achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(hbm_achieved / HBM_PEAK_GBS, 5), 'traffic': None,
            'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note}
-    # K2: the library runs the band-loop kernel for launches of >= 8,192
-    # images (FFCV_K2_LOOP=1: always, =0: never), the per-band one otherwise;
-    # the per-kernel roofline names the one its isolated launches (cap images,
-    # as the rocprofv3 passes' uniform launches) ran
+    # K2: the library runs the per-band kernel at every launch size, the
+    # band-loop one only with FFCV_K2_LOOP=1 (an A/B knob since round 5)
     k2e = os.environ.get('FFCV_K2_LOOP')
-    k2_min = 8192 if k2e is None else (0 if k2e.strip() not in ('0', '') else 1 << 62)
+    k2_min = 0 if k2e is not None and k2e.strip() not in ('0', '') else 1 << 62
     k2_loop = cap >= k2_min
     k2 = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>' if k2_loop else
           f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')

@@ -3409,13 +3409,14 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   {
     const char *o = getenv("FFCV_K1_ORDER");  // size-grouped K1 workgroups (A/B knob: 0 turns it off)
     c->k1_sorted = !o || atoi(o) != 0;
-    // band-loop K2 for launches of at least k2_loop_min images (DESIGN.md s6,
-    // round 4: +2.8% at C3's 12,288-image launches, -9% at the driver's
-    // 2,048-4,096: with few images per launch its long workgroups hold LDS the
-    // other streams' entropy workgroups wait for, and end the launch in a
-    // coarser tail).  FFCV_K2_LOOP=0 never, =1 always, unset: the size rule
+    // the band-loop K2 (jpeg_rrc_loop_kernel) only when FFCV_K2_LOOP=1 (A/B
+    // knob).  Round 4 ran it for launches of >= 8,192 images (+2.8% then at
+    // C3's 12,288-image launches, -9% at the driver's 2,048-4,096); since
+    // round 5 the per-band kernel is as fast at 12,288 too (3.10 M vs
+    // 3.09-3.10 M at 400 steps; 135 vs 165-168 ns per image alone, DESIGN.md
+    // s6), so every launch size runs the per-band kernel
     const char *l = getenv("FFCV_K2_LOOP");
-    c->k2_loop_min = !l ? 8192 : (atoi(l) != 0 ? 0 : INT_MAX);
+    c->k2_loop_min = l && atoi(l) != 0 ? 0 : INT_MAX;
   }
   c->max_h = max_height;
   c->max_w = max_width;

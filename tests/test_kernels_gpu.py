@@ -381,9 +381,9 @@ def test_jpeg_rrc_matches_oracle(hip_lib, oracle, out_hw, k2_loop, monkeypatch):
     300 has out_w + out_h past K2_TAPS, where K1 writes no tap table and K2
     must not read one (the prefetch read past the allocation).
     Both colour / resize kernels: the per-band one and the band-loop one
-    (FFCV_K2_LOOP=1 forces it; the library picks it for launches of >= 8,192
-    images), whose general path serves the 4:2:2 / 4:4:4 / grey images and
-    the area-resize crops of this set."""
+    (FFCV_K2_LOOP=1 selects it: an A/B knob since round 5), whose general
+    path serves the 4:2:2 / 4:4:4 / grey images and the area-resize crops of
+    this set."""
     monkeypatch.setenv('FFCV_K2_LOOP', k2_loop)  # read when the context is made
     OH, OW = out_hw
     torch = _torch()

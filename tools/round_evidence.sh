@@ -23,19 +23,6 @@ fi
 # every profiled launch the same size (C3 / C2: 24 batches per launch, warmup = one launch)
 bash tools/profile.sh ${TAG}_c3 --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c3 12288 gpurun_out/${TAG}_c3_summary.json gpurun_out/traffic_c3.json gpurun_out/sq_c3.json > /dev/null
-# the per-band K2 the driver's launches (< 8,192 images) run: the same passes
-# with FFCV_K2_LOOP=0, merged into sq_c3.json / traffic_c3.json
-FFCV_K2_LOOP=0 bash tools/profile.sh ${TAG}_c3pb --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches
-python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c3pb 12288 gpurun_out/${TAG}_c3pb_summary.json gpurun_out/traffic_c3pb.json gpurun_out/sq_c3pb.json > /dev/null
-python3 - <<'PY'
-import json
-for k in ('traffic', 'sq'):
-    a = json.load(open(f'gpurun_out/{k}_c3.json')); b = json.load(open(f'gpurun_out/{k}_c3pb.json'))
-    for n, v in b.items():
-        if n.startswith('jpeg_color_resize_kernel'):
-            a[n] = v
-    json.dump(a, open(f'gpurun_out/{k}_c3.json', 'w'), indent=1, sort_keys=True)
-PY
 bash tools/profile.sh ${TAG}_c2 --config c2 --unique 10000 --steps 48 --warmup 24 --no-cpu-baseline --uniform-launches
 python3 tools/pmc_summary.py gpurun_out/prof_${TAG}_c2 6144 gpurun_out/${TAG}_c2_summary.json gpurun_out/traffic_c2.json gpurun_out/sq_c2.json > /dev/null
 # C5 launches one at a time (--inflight 1): the profile's avg_ns is then the

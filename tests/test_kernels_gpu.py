@@ -176,6 +176,43 @@ def test_raw_rrc_matches_oracle(hip_lib, oracle):
         assert np.array_equal(got.view(np.uint16), want.view(np.uint16))
 
 
+def test_raw_rrc_area_walk(hip_lib, oracle):
+    """The raw kernel's INTER_AREA walk for scales in [1, 2) (round 5: four
+    columns per thread, aligned 4-byte LDS reads shifted by v_alignbyte, one
+    cached source row): crops at every byte alignment of their first pixel
+    and row (offsets and widths over 0..3 mod 4), scales from just above 1 to
+    just below 2 on either axis, the 448 (C5) and 224 outputs and a 220-wide
+    one, with flip + cutout (both orders) + fp16 LUT.  Bit-exact."""
+    rng = np.random.default_rng(77)
+    B = 40
+    imgs = [natural_image(rng, 520, 530) for _ in range(B)]
+    crops = []
+    for k in range(B):
+        if k < 16:  # 448 out: scales in [1, 1.18)
+            h, w = 448 + int(rng.integers(0, 72)), 448 + int(rng.integers(0, 82))
+        else:       # 224 / 220 out: scales in [1, 2)
+            h, w = 224 + int(rng.integers(0, 220)), 224 + int(rng.integers(0, 220))
+        i, j = int(rng.integers(0, 520 - h + 1)), int(rng.integers(0, 530 - w + 1))
+        j = j - (j % 4) + k % 4 if j - (j % 4) + k % 4 + w <= 530 else j  # every alignment of the first byte
+        crops.append((i, j, h, w))
+    crops = np.array(crops, np.int32)
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    for sel, out in ((slice(0, 16), (448, 448)), (slice(16, B), (224, 224)), (slice(16, B), (224, 220))):
+        im, cr = imgs[sel], crops[sel]
+        n = len(im)
+        u8 = oracle.rrc_batch([(x.reshape(-1), x.shape[0], x.shape[1], 1) for x in im], cr, *out)
+        got = _run_raw_rrc(hip_lib, im, cr, out)
+        bad = np.argwhere((got != u8).reshape(n, -1).any(1)).ravel()
+        assert bad.size == 0, f'{out}: samples {bad[:8]} differ; crops {cr[bad[:4]]}'
+        cs = min(out) // 4
+        cut = np.stack([rng.integers(0, out[0] - cs + 1, n), rng.integers(0, out[1] - cs + 1, n)], 1).astype(np.int32)
+        flips = (np.arange(n) % 2).astype(np.uint8)
+        for cbf in (False, True):
+            got = _run_raw_rrc(hip_lib, im, cr, out, cut, cs, (124, 116, 103), flips, lut, cbf)
+            want = _oracle_post(u8, flips, cut, cs, (124, 116, 103), lut, cbf)
+            assert np.array_equal(got.view(np.uint16), want.view(np.uint16)), (out, cbf)
+
+
 def test_raw_rrc_448_c5(hip_lib, oracle):
     """C5 shapes through the LDS-staged bands: device draws over 512x512
     sources (linear and area crops), plus a full-frame area crop, odd-offset

@@ -2369,6 +2369,7 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
   int row0;
   int step;
   FFCV_DEV int at(int y, int x, int c) const { return p[__mul24(y - row0, step) + x * 3 + c]; }
+  FFCV_DEV const uint8_t *pix(int y, int x) const { return p + __mul24(y - row0, step) + x * 3; }
 };
 
 #ifndef K2_WPE
@@ -2888,6 +2889,8 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
     __syncthreads();
   }
   LdsRoi lr{roi, r0, step};
+  // resize_area_lds reads up to 5 bytes past the staged rows
+  const bool pad8 = (int)(roi - lds) + nrows * step + 8 <= LDS_BYTES;
   RoiSrc gr{groi, (uint64_t)step};
   auto px = [&](int dy, int dx, int v[3]) {
     if (ep.in_cut(dy, dx)) {
@@ -2908,7 +2911,9 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       }
     } else if (staged && tabs) {
       const int cx = ep.src_x(dx);
-      if (P.kind == 2)
+      if (P.kind == 2 && pad8)  // (aligned reads: see resize_area_lds)
+        resize_area_lds(lr, atab[cx], atab[out_w + dy - oy0], v);
+      else if (P.kind == 2)
         resize_area(lr, atab[cx], atab[out_w + dy - oy0], v);
       else
         resize_linear(P, lr, cx, ltab[cx], ltab[out_w + dy - oy0], v);

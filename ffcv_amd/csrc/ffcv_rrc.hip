@@ -70,6 +70,7 @@ struct LdsSrc {
     return p + r * pitch + ((lead + r * stepmod) & 15);
   }
   FFCV_DEV int at(int y, int x, int c) const { return row(y)[x * 3 + c]; }
+  FFCV_DEV const uint8_t *pix(int y, int x) const { return row(y) + x * 3; }
 };
 
 // One workgroup per band of RRC_BAND output rows of one image.
@@ -341,7 +342,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         const AreaTaps ty = s_at[dy - oy0];
         int v[12];
 #pragma unroll
-        for (int j = 0; j < 4; j++) resize_area(L, tx[j], ty, v + 3 * j);
+        for (int j = 0; j < 4; j++) resize_area_lds(L, tx[j], ty, v + 3 * j);  // (s_src is followed by s_rt: in LDS)
         put(dy, v);
       }
       return;

@@ -1329,9 +1329,12 @@ FFCV_DEV uint64_t eidx_hash(uint32_t w0, uint32_t w1, uint32_t w2, int t) {
 // stores and the IDCT's block reads reach them (zeroed at allocation, ~300 us
 // earlier, they had been written back and the stores missed).
 FFCV_DEV void zero_window_coefs(const JShared &S, int16_t *coef, int t) {
-  uint4 *cz = wave_uniform((uint4 *)coef);
+  // (a global-address-space pointer: global_store, not flat_store, which
+  // would also count in lgkmcnt)
+  typedef __attribute__((address_space(1))) u32x4_t gu4_t;
+  gu4_t *cz = (gu4_t *)(uintptr_t)wave_uniform((uint4 *)coef);
   const uint32_t n = wuni((uint32_t)(S.nwin * 8));
-  for (uint32_t i = (uint32_t)t; i < n; i += JL) cz[i] = make_uint4(0, 0, 0, 0);
+  for (uint32_t i = (uint32_t)t; i < n; i += JL) cz[i] = (u32x4_t){0u, 0u, 0u, 0u};
   wsync_mem();
 }
 

@@ -182,9 +182,16 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
           const uint64_t ra = row0 + (uint64_t)r * src.step;
           // chunks holding bytes of this row (none past the dataset's end)
           const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
-          const uint4 *rp = (const uint4 *)(uintptr_t)(ra & ~(uint64_t)15) + cg;
-          v[q][0] = ln < lim ? rp[ln] : make_uint4(0, 0, 0, 0);
-          v[q][1] = ln + 64 < lim ? rp[ln + 64] : make_uint4(0, 0, 0, 0);
+          // (a global-address-space pointer: global_load, not flat_load --
+          // a flat load also counts in lgkmcnt, so every LDS wait would wait
+          // for it too)
+          typedef const __attribute__((address_space(1))) uint32_t gu32_t;
+          gu32_t *rp = (gu32_t *)(uintptr_t)(ra & ~(uint64_t)15) + 4 * cg;
+          uint4 a = make_uint4(0, 0, 0, 0), b = a;
+          if (ln < lim) a = make_uint4(rp[4 * ln], rp[4 * ln + 1], rp[4 * ln + 2], rp[4 * ln + 3]);
+          if (ln + 64 < lim) b = make_uint4(rp[4 * ln + 256], rp[4 * ln + 257], rp[4 * ln + 258], rp[4 * ln + 259]);
+          v[q][0] = a;
+          v[q][1] = b;
         }
 #pragma unroll
         for (int q = 0; q < RRC_STAGE_ROWS; q++) {

@@ -70,7 +70,7 @@
 #ifndef FB_AC
 #define FB_AC 11        // first-level bits, the scan's first AC table (luma)
 #endif
-static_assert(FB_AC <= 11, "make_pair's entries hold code + extra bits of at most 11 bits (a 12-bit build decoded wrong)");
+static_assert(FB_AC <= 11, "FB_AC > 11 is not supported: a 12-bit build failed the bench parity check (DESIGN.md s6, r6j)");
 #define FB_AC2 10       // first-level bits, further AC tables (chroma)
 #ifndef FB_DC
 #define FB_DC 8         // first-level bits, DC tables

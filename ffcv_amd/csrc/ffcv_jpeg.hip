@@ -2376,6 +2376,23 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
   FFCV_DEV const uint8_t *pix(int y, int x) const { return p + __mul24(y - row0, step) + x * 3; }
 };
 
+// K2's FP16 LUT in LDS is channel-major, [c][256] halves (a.p.lut is [v][c]):
+// entry (v, c) is v shifted plus the ds_read's immediate offset c * 512,
+// where the interleaved v * 3 + c compiled to a 64-bit multiply-add per read
+typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
+FFCV_DEV uint32_t lut_at(const lds_u16_t *L, int v, int c) { return L[(uint32_t)v + 256u * (uint32_t)c]; }
+FFCV_DEV uint16_t lut_src(const uint16_t *lut, int d) { return lut[(d & 255) * 3 + (d >> 8)]; }  // LDS entry d
+// The linear walk's last step, VResizeLinearVec's (m0 + m1 + 2) >> 2 of the
+// vertical sum x = m0 + m1: the u8 value, or (FP16) the LDS byte address of
+// its channel-0 LUT entry, base + 2 * ((x + 2) >> 2) = (x + lq) >> 1 & ~1 with
+// lq = 2 + 2 * base (base even): an add3, a shift and an and, where indexing
+// the value cost a 4-cycle shift-add more (tools/op_rate); lut_ld reads the
+// channel-c entry at that address (channel c's table: + 512 c bytes)
+template <bool FP16>
+FFCV_DEV uint32_t lut_q(uint32_t x, uint32_t lq) { return FP16 ? ((x + lq) >> 1) & ~1u : (x + 2u) >> 2; }
+FFCV_DEV uint32_t lut_base(const lds_u16_t *L) { return (uint32_t)(uintptr_t)L; }
+FFCV_DEV uint32_t lut_ld(uint32_t q, int c) { return ((const lds_u16_t *)(uintptr_t)q)[256 * c]; }
+
 #ifndef K2_WPE
 #define K2_WPE 6  // waves per SIMD K2 is compiled for (6 WGs per CU at K2_LDS)
 #endif
@@ -2385,7 +2402,7 @@ struct LdsRoi {  // crop rows [row0, row0 + nrows), staged as RGB in LDS
 // the only thread-level return follows the last one.
 template <int MODE, bool FP16, bool GENERAL_ONLY = false, int LDS_BYTES = K2_LDS>
 FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *lds) {
-  uint16_t *s_lut = (uint16_t *)lds;  // 768 entries (FP16)
+  lds_u16_t *s_lut = (lds_u16_t *)lds;  // 768 entries (FP16), channel-major
   const int t = threadIdx.x;
   // ---- one round trip for everything that depends only on (k, band, t):
   // the record head, the LUT, this band's row taps, this thread's column
@@ -2396,7 +2413,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   uint16_t lv[LU];
   if (FP16) {
 #pragma unroll
-    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? a.p.lut[u * K2T + t] : (uint16_t)0;
+    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? lut_src(a.p.lut, u * K2T + t) : (uint16_t)0;
   }
   const int band_rows_n = MODE == JM_RRC ? min(a.p.out_h - band * BAND, BAND) : 0;
   // K1 writes an image's tap table only when out_w + out_h fits K2_TAPS: a
@@ -2522,7 +2539,12 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
     if (need <= LDS_BYTES) {
       K2_STOP_AT(1, a.out_stride != 77);  // diagnostics: the band's set-up (record, LUT, taps, tile bounds)
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
-      if (t < oy1 - oy0) rtab[t] = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+      if (t < oy1 - oy0) {  // weights stored as the walk's multiplier operands, c << 8 (see hrow)
+        LinTap lt = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
+        lt.c0 = (lt.c0 & 0xfff) << 8;
+        lt.c1 = (lt.c1 & 0xfff) << 8;
+        rtab[t] = lt;
+      }
       TPlane tp[3];
       // tile staging: the first SU dwords per thread of every component are
       // loaded before any LDS write (one memory round trip, not one per
@@ -2658,9 +2680,9 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
         l1 = lin_tap(P.scale_x, P.inv_x, P.sw, ep.src_x(dx0 + 1));
       }
       // a border tap (src[s] * 2048) as the same two-tap form with weights
-      // (2048, 0) on (s, s): branch-free, identical sums
-      const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
-      const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
+      // (2048, 0) on (s, s + 1): branch-free, identical sums
+      const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1;
+      const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1;
       // horizontal pass of crop row r for both columns: sat_s16(h >> 4) per
       // channel.  The saturations of this walk never act (so they are not
       // computed): weights are in [0, 2048] with c0 + c1 <= 2049 (linear_coef
@@ -2676,10 +2698,15 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       // v_dot2_u32_u16 with the weights pre-scaled by 16: dot = 16 h, and
       // (h >> 4) << 8 = dot & 0x7fff00 (10 cycles per value instead of 22).
       const uint32_t w0 = ((uint32_t)a0w << 4) | ((uint32_t)b0w << 20), w1 = ((uint32_t)a1w << 4) | ((uint32_t)b1w << 20);
+      const uint32_t so0 = 4u * (uint32_t)l0.s, so1 = 4u * (uint32_t)l1.s;  // byte offsets in a row
       auto hrow = [&](int r, uint32_t H[6]) {
         const uint32_t *row = rgbx + __mul24(r - r0, rw);
-        const uint32_t p0 = row[l0.s], q0 = row[s0b];
-        const uint32_t p1 = row[l1.s], q1 = row[s1b];
+        // words s and s + 1 as one ds_read2 per column (a border tap's second
+        // word has weight 0: at the crop's right edge it is the next row's
+        // first word or, in the last row, the dummy word)
+        const uint32_t *e0 = (const uint32_t *)((const uint8_t *)row + so0), *e1 = (const uint32_t *)((const uint8_t *)row + so1);
+        const uint32_t p0 = e0[0], q0 = e0[1];
+        const uint32_t p1 = e1[0], q1 = e1[1];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
           // bytes [p.c, 0, q.c, 0]: v_perm_b32 selector c | 0x0c << 8 | (4 + c) << 16 | 0x0c << 24
@@ -2696,6 +2723,9 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       // cutout: which of this thread's two columns lie in the square (tested
       // once; a row tests its own range)
       const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
+      const uint32_t lq = FP16 ? 2u + 2u * lut_base(s_lut) : 2u;  // (lut_q)
+      uint32_t qfill[3];  // the cutout fill as lut_q's result
+      for (int c = 0; c < 3; c++) qfill[c] = FP16 ? lut_base(s_lut) + 2u * ep.fill[c] : ep.fill[c];
       const int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
       // (a row group is two whole waves: its rows are wave-uniform, so the
       // per-row tap read, cutout test and row changes are scalar)
@@ -2719,27 +2749,27 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
           hrow(rb, HB);
           cb = rb;
         }
-        int o[6];
-        const uint32_t c0 = ((uint32_t)ly.c0 & 0xfffu) << 8, c1 = ((uint32_t)ly.c1 & 0xfffu) << 8;
+        uint32_t o[6];
+        const uint32_t c0 = ly.c0, c1 = ly.c1;  // (pre-scaled in rtab)
 #pragma unroll
-        for (int i = 0; i < 6; i++)  // (sat_s16(m0 + m1) + 2) >> 2, no saturation (see hrow)
-          o[i] = (int)((mulhi24(HA[i], c0) + mulhi24(HB[i], c1) + 2u) >> 2);
+        for (int i = 0; i < 6; i++)  // (sat_s16(m0 + m1) + 2) >> 2, no saturation (see hrow); FP16: its LUT address
+          o[i] = lut_q<FP16>(mulhi24(HA[i], c0) + mulhi24(HB[i], c1), lq);
         if ((cut0 || cut1) && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
           if (cut0) {
-            o[0] = ep.fill[0];
-            o[1] = ep.fill[1];
-            o[2] = ep.fill[2];
+            o[0] = qfill[0];
+            o[1] = qfill[1];
+            o[2] = qfill[2];
           }
           if (cut1) {
-            o[3] = ep.fill[0];
-            o[4] = ep.fill[1];
-            o[5] = ep.fill[2];
+            o[3] = qfill[0];
+            o[4] = qfill[1];
+            o[5] = qfill[2];
           }
         }
         const uint64_t p0 = (uint64_t)dy * out_w + dx0;
         if (FP16) {
-          const uint32_t h0 = s_lut[o[0] * 3], h1 = s_lut[o[1] * 3 + 1], h2 = s_lut[o[2] * 3 + 2];
-          const uint32_t h3 = s_lut[o[3] * 3], h4 = s_lut[o[4] * 3 + 1], h5 = s_lut[o[5] * 3 + 2];
+          const uint32_t h0 = lut_ld(o[0], 0), h1 = lut_ld(o[1], 1), h2 = lut_ld(o[2], 2);
+          const uint32_t h3 = lut_ld(o[3], 0), h4 = lut_ld(o[4], 1), h5 = lut_ld(o[5], 2);
           typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));  // 12-byte group, 4-byte aligned
           u32x3 w;
           w.x = h0 | (h1 << 16);
@@ -2941,10 +2971,10 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
     if (two) px(dy, dx + 1, u);
     const uint64_t p0 = (uint64_t)dy * out_w + dx;
     if (FP16) {
-      uint16_t h0 = s_lut[v[0] * 3], h1 = s_lut[v[1] * 3 + 1], h2 = s_lut[v[2] * 3 + 2];
+      uint16_t h0 = lut_at(s_lut, v[0], 0), h1 = lut_at(s_lut, v[1], 1), h2 = lut_at(s_lut, v[2], 2);
       uint16_t *o = (uint16_t *)ob + p0 * 3;
       if (two) {
-        uint16_t h3 = s_lut[u[0] * 3], h4 = s_lut[u[1] * 3 + 1], h5 = s_lut[u[2] * 3 + 2];
+        uint16_t h3 = lut_at(s_lut, u[0], 0), h4 = lut_at(s_lut, u[1], 1), h5 = lut_at(s_lut, u[2], 2);
         uint32_t *o32 = (uint32_t *)o;  // p0 even -> 12-byte aligned group
         o32[0] = h0 | ((uint32_t)h1 << 16);
         o32[1] = h2 | ((uint32_t)h3 << 16);
@@ -3059,7 +3089,7 @@ template <bool FP16>
 __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WPE))) jpeg_rrc_loop_kernel(JpegArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ __attribute__((aligned(16))) uint32_t s_tile[K2L_TILE / 4];
-  uint16_t *s_lut = (uint16_t *)lds;
+  lds_u16_t *s_lut = (lds_u16_t *)lds;  // channel-major (lut_at)
   const int t = threadIdx.x;
   const int k = blockIdx.y;
   const int out_h = a.p.out_h, out_w = a.p.out_w;
@@ -3071,7 +3101,7 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   uint16_t lv[LU];
   if (FP16) {
 #pragma unroll
-    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? a.p.lut[u * K2T + t] : (uint16_t)0;
+    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? lut_src(a.p.lut, u * K2T + t) : (uint16_t)0;
   }
   const uint2 *ktaps = a.taps && out_w + out_h <= K2_TAPS ? a.taps + (uint64_t)k * K2_TAPS : nullptr;
   uint4 ct_pre = make_uint4(0, 0, 0, 0);
@@ -3146,10 +3176,14 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
   const bool walker = tx < out_w / 2;
   const int dx0 = 2 * tx;
   const LinTap l0 = tap_unpack(make_uint2(ct_pre.x, ct_pre.y)), l1 = tap_unpack(make_uint2(ct_pre.z, ct_pre.w));
-  const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1, s0b = l0.border ? l0.s : l0.s + 1;
-  const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1, s1b = l1.border ? l1.s : l1.s + 1;
+  const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1;
+  const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1;
   const uint32_t w0 = ((uint32_t)a0w << 4) | ((uint32_t)b0w << 20), w1 = ((uint32_t)a1w << 4) | ((uint32_t)b1w << 20);
+  const uint32_t so0 = 4u * (uint32_t)l0.s, so1 = 4u * (uint32_t)l1.s;  // byte offsets in a row
   const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
+  const uint32_t lq = FP16 ? 2u + 2u * lut_base(s_lut) : 2u;  // (lut_q)
+  uint32_t qfill[3];  // the cutout fill as lut_q's result
+  for (int c = 0; c < 3; c++) qfill[c] = FP16 ? lut_base(s_lut) + 2u * ep.fill[c] : ep.fill[c];
   constexpr int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
   // the counted wait below sets vmcnt's low field only (gfx9: 4 bits; the
   // bits above it are expcnt / lgkmcnt); tests/test_isa_guards.py checks on
@@ -3280,8 +3314,12 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
     if (walker) {
       auto hrow = [&](int r, uint32_t H[6]) {
         const uint32_t *row = rgbx + __mul24(r - r0, rw);
-        const uint32_t p0 = row[l0.s], q0 = row[s0b];
-        const uint32_t p1 = row[l1.s], q1 = row[s1b];
+        // words s and s + 1 as one ds_read2 per column (a border tap's second
+        // word has weight 0: at the crop's right edge it is the next row's
+        // first word or, in the last row, the dummy word)
+        const uint32_t *e0 = (const uint32_t *)((const uint8_t *)row + so0), *e1 = (const uint32_t *)((const uint8_t *)row + so1);
+        const uint32_t p0 = e0[0], q0 = e0[1];
+        const uint32_t p1 = e1[0], q1 = e1[1];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
           const uint32_t sel = (uint32_t)c | 0x0c00u | ((uint32_t)(4 + c) << 16) | 0x0c000000u;
@@ -3312,26 +3350,26 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WP
           hrow(rb, HB);
           cb = rb;
         }
-        int o[6];
+        uint32_t o[6];
         const uint32_t c0 = ((uint32_t)ly.c0 & 0xfffu) << 8, c1 = ((uint32_t)ly.c1 & 0xfffu) << 8;
 #pragma unroll
-        for (int i = 0; i < 6; i++) o[i] = (int)((mulhi24(HA[i], c0) + mulhi24(HB[i], c1) + 2u) >> 2);
+        for (int i = 0; i < 6; i++) o[i] = lut_q<FP16>(mulhi24(HA[i], c0) + mulhi24(HB[i], c1), lq);
         if ((cut0 || cut1) && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
           if (cut0) {
-            o[0] = ep.fill[0];
-            o[1] = ep.fill[1];
-            o[2] = ep.fill[2];
+            o[0] = qfill[0];
+            o[1] = qfill[1];
+            o[2] = qfill[2];
           }
           if (cut1) {
-            o[3] = ep.fill[0];
-            o[4] = ep.fill[1];
-            o[5] = ep.fill[2];
+            o[3] = qfill[0];
+            o[4] = qfill[1];
+            o[5] = qfill[2];
           }
         }
         const uint64_t p0 = (uint64_t)dy * out_w + dx0;
         if (FP16) {
-          const uint32_t h0 = s_lut[o[0] * 3], h1 = s_lut[o[1] * 3 + 1], h2 = s_lut[o[2] * 3 + 2];
-          const uint32_t h3 = s_lut[o[3] * 3], h4 = s_lut[o[4] * 3 + 1], h5 = s_lut[o[5] * 3 + 2];
+          const uint32_t h0 = lut_ld(o[0], 0), h1 = lut_ld(o[1], 1), h2 = lut_ld(o[2], 2);
+          const uint32_t h3 = lut_ld(o[3], 0), h4 = lut_ld(o[4], 1), h5 = lut_ld(o[5], 2);
           typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
           u32x3 w;
           w.x = h0 | (h1 << 16);

@@ -172,10 +172,13 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     // l + 64: the row address and its chunk count are wave-uniform (scalar),
     // a lane's chunk offset is fixed, and a wave has up to RRC_STAGE_ROWS
     // rows' loads in flight before its LDS writes
-    const int wv = t >> 6, ln = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;  // (wv scalar: row addresses in SGPRs)
+    // (a lane that loads nothing keeps the registers' previous contents: its
+    // LDS write is skipped too; zeroing them cost 8 moves per row)
+    typedef uint32_t sx4_t __attribute__((ext_vector_type(4)));
+    sx4_t v[RRC_STAGE_ROWS][2] = {};
     for (int cg = 0; cg < nch; cg += 128)  // (one pass for rows up to 2 KB: crops up to 677 px wide)
       for (int rb0 = wv; rb0 < nrows; rb0 += 4 * RRC_STAGE_ROWS) {
-        uint4 v[RRC_STAGE_ROWS][2];
 #pragma unroll
         for (int q = 0; q < RRC_STAGE_ROWS; q++) {
           const int r = rb0 + 4 * q;
@@ -187,19 +190,16 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
           // for it too)
           typedef const __attribute__((address_space(1))) uint32_t gu32_t;
           gu32_t *rp = (gu32_t *)(uintptr_t)(ra & ~(uint64_t)15) + 4 * cg;
-          uint4 a = make_uint4(0, 0, 0, 0), b = a;
-          if (ln < lim) a = make_uint4(rp[4 * ln], rp[4 * ln + 1], rp[4 * ln + 2], rp[4 * ln + 3]);
-          if (ln + 64 < lim) b = make_uint4(rp[4 * ln + 256], rp[4 * ln + 257], rp[4 * ln + 258], rp[4 * ln + 259]);
-          v[q][0] = a;
-          v[q][1] = b;
+          if (ln < lim) v[q][0] = (sx4_t){rp[4 * ln], rp[4 * ln + 1], rp[4 * ln + 2], rp[4 * ln + 3]};
+          if (ln + 64 < lim) v[q][1] = (sx4_t){rp[4 * ln + 256], rp[4 * ln + 257], rp[4 * ln + 258], rp[4 * ln + 259]};
         }
 #pragma unroll
         for (int q = 0; q < RRC_STAGE_ROWS; q++) {
           const int r = rb0 + 4 * q;
           const uint64_t ra = row0 + (uint64_t)r * src.step;
           const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
-          if (ln < lim) s_src[r * nch + cg + ln] = v[q][0];
-          if (ln + 64 < lim) s_src[r * nch + cg + ln + 64] = v[q][1];
+          if (ln < lim) s_src[r * nch + cg + ln] = __builtin_bit_cast(uint4, v[q][0]);
+          if (ln + 64 < lim) s_src[r * nch + cg + ln + 64] = __builtin_bit_cast(uint4, v[q][1]);
         }
       }
   }

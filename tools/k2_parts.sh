@@ -7,7 +7,7 @@ TAG=$1; V=${2:-"new k2stop1 k2stop2 k2stop3"}
 export TMPDIR=/tmp FFCV_K2_LOOP=0
 # warm the box first (first import of torch, the /tmp sample cache) with
 # output going to a file: a profiled run that is silent for 3 minutes is killed
-timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --parity-rows 0 --no-kernel-events --no-later-epochs --no-c5 > gpurun_out/${TAG}_warm.log 2>&1 || { tail -3 gpurun_out/${TAG}_warm.log; exit 1; }
+timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 --no-host-check --no-cpu-baseline --parity-rows 0 --no-kernel-events --no-later-epochs --no-c5 > gpurun_out/${TAG}_warm.log 2>&1 || { tail -3 gpurun_out/${TAG}_warm.log; exit 1; }
 for v in $V; do
   lib=""; [ $v != new ] && lib="--lib build/ab/$v.so"
   d=gpurun_out/${TAG}_$v

@@ -490,6 +490,49 @@ def test_jpeg_rrc_edge_crops(hip_lib, oracle):
     assert bad.size == 0, f'samples {bad} differ'
 
 
+def test_jpeg_rrc_corner_upscale_fp16_cutout(hip_lib, oracle):
+    """K2's linear walk at its edges, through the FP16 LUT: tiny crops in the
+    image's corners upscaled to 224 (every column near the right edge is a
+    border tap, whose zero-weight second word the walk reads past the crop
+    row: the next row or, in the band's last row, the dummy word), cutout
+    squares over the corners (the fill as a LUT address, lut_q) and both
+    flips."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(91)
+    shapes = [(64, 64), (64, 64), (37, 53), (37, 53), (256, 256), (256, 256), (90, 17), (17, 90)]
+    imgs = [natural_image(rng, h, w) for h, w in shapes]
+    blobs = [encode_jpeg(im, 85, '4:2:0') for im in imgs]
+    # (y, x, h, w): bottom-right / top-left / right-edge corners, 2 x 2 to 13 x 11
+    crops = np.array([[62, 62, 2, 2], [0, 0, 3, 5], [34, 48, 3, 5], [0, 50, 13, 3], [249, 245, 7, 11],
+                      [200, 255, 9, 1], [80, 9, 10, 8], [5, 79, 12, 11]], np.int32)
+    B = len(imgs)
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    dec = L.JpegDecoder(B, max(h for h, _ in shapes), max(w for _, w in shapes), max(len(b) for b in blobs))
+    u8 = oracle.rrc_batch([(b, h, w, 0) for b, (h, w) in zip(blobs, shapes)], crops, 224, 224)
+    flips = (np.arange(B) % 2).astype(np.uint8)
+    cut = np.array([[224 - 40, 224 - 40], [0, 0], [100, 200], [200, 100], [0, 192], [192, 0], [96, 96], [223, 223]],
+                   np.int32)
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    p = L.RRCParams()
+    p.out_h, p.out_w = 224, 224
+    p.cutout_size = 40
+    for i, f in enumerate((255, 0, 17)):
+        p.cutout_fill[i] = f
+    d_lut = torch.from_numpy(lut.view(np.int16)).to('cuda:0')
+    p.lut = d_lut.data_ptr()
+    out = torch.zeros((B, 224, 224, 3), dtype=torch.float16, device='cuda:0')
+    status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+    dec.rrc(d_buf, d_smp, B, torch.from_numpy(crops).to('cuda:0'), torch.from_numpy(cut).to('cuda:0'),
+            torch.from_numpy(flips).to('cuda:0'), p, out, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    want = _oracle_post(u8, flips, cut, 40, (255, 0, 17), lut)
+    got = out.cpu().numpy()
+    bad = np.argwhere((got.view(np.uint8) != want.view(np.uint8)).reshape(B, -1).any(1)).ravel()
+    assert bad.size == 0, f'samples {bad} differ'
+
+
 def test_jpeg_corrupt_and_unsupported(hip_lib, oracle):
     torch = _torch()
     from ffcv_amd import libffcv as L

@@ -16,9 +16,8 @@ descriptor gather, crop/cutout draws, parse, de-stuff, parallel Huffman
 decode of the crop's coefficients), jpeg_idct_kernel (K1b: DC prediction,
 dequantise + ifast IDCT of the crop's blocks) and jpeg_color_resize_kernel
 (K2: upsample + colour, INTER_AREA, cutout, LUT; one workgroup per 16-row
-band; the band-loop jpeg_rrc_loop_kernel only with FFCV_K2_LOOP=1).  The
-1.28M-entry dataset
-is built from U unique encodings replicated at distinct HBM addresses.
+band).  The 1.28M-entry dataset is built from U unique encodings replicated
+at distinct HBM addresses.
 
 After the timed region (outside it) the rows each slot's last timed launch
 wrote are compared bit for bit with the oracle (parity_check); the line's
@@ -840,20 +839,11 @@ def main():
     hbm = {'bound': 'hbm', 'achieved': round(hbm_achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(hbm_achieved / HBM_PEAK_GBS, 5), 'traffic': None,
            'algorithmic_bytes_per_image': round(unit_bytes, 1), 'note': roof_note}
-    # K2: the library runs the per-band kernel at every launch size, the
-    # band-loop one only with FFCV_K2_LOOP=1 (an A/B knob since round 5)
-    k2e = os.environ.get('FFCV_K2_LOOP')
-    k2_min = 0 if k2e is not None and k2e.strip() not in ('0', '') else 1 << 62
-    k2_loop = cap >= k2_min
-    k2 = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>' if k2_loop else
-          f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
+    # K2: the per-band kernel at every launch size (the band-loop form was
+    # deleted in round 6)
+    k2 = f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>'
     kernels = ['jpeg_entropy_kernel<0>', 'jpeg_idct_kernel', k2] if mode == 'jpg' else ['rrc_raw_kernel<false>']
-    # the timed launches' own K2 (the driver's 20 steps: launches of 2,048-4,096
-    # images, the per-band kernel) for the whole-path figures (path, traffic)
-    k2t = (f'jpeg_rrc_loop_kernel<{"true" if norm else "false"}>'
-           if max(launch_imgs) >= k2_min else
-           f'jpeg_color_resize_kernel<0, {"true" if norm else "false"}>')
-    timed_kernels = kernels[:2] + [k2t] if mode == 'jpg' else kernels
+    timed_kernels = kernels
     # HBM traffic of the same kernels from the committed rocprofv3 PMC passes
     # (tools/profile.sh -> tools/pmc_summary.py): bytes per image x images per launch
     pm = load_profile(f'traffic_{args.config}.json')
@@ -998,6 +988,11 @@ def main():
                                 if 'hbm_bytes_per_image_counter' in d else None),
                     'hbm_frac_recipe': d.get('hbm_frac_alg_profile'),
                     'issue_frac_4cyc': d['issue_frac'], 'issue_frac_2cyc': d['issue_frac_2cyc'],
+                    # frac is the contract's HBM fraction; the resource that
+                    # binds these kernels is VALU issue (named, so
+                    # round-over-round readers compare like with like)
+                    'binding': {'resource': 'VALU issue', 'frac_4cyc': d['issue_frac'],
+                                'frac_2cyc': d['issue_frac_2cyc'], 'path_frac_4cyc': roof['frac']},
                     'issue_achieved': round(d['valu_per_image'] / d['ns_per_image_isolated'], 2),
                     'issue_unit': 'G VALU wave-instr/s',
                     'dominant_kernel': dom, **launch,

@@ -65,6 +65,7 @@
 #ifndef JL
 #define JL 64           // lanes per image: a wave decodes JT / JL images side by side
 #endif
+static_assert(JL == JT, "JL != 64 is not maintained: a round-5 -DJL=32 build was 10% slower and not bit-exact (profiles/r5b_ab20_jl32.log)");
 #define IPW (JT / JL)   // images per wave
 #define HDR_BYTES 2048  // header bytes staged in LDS (aliased by the LUT pool)
 #ifndef FB_AC
@@ -2396,11 +2397,11 @@ FFCV_DEV uint32_t lut_ld(uint32_t q, int c) { return ((const lds_u16_t *)(uintpt
 #ifndef K2_WPE
 #define K2_WPE 6  // waves per SIMD K2 is compiled for (6 WGs per CU at K2_LDS)
 #endif
-// One band of BAND output rows of image k (the per-band K2 below runs one per
-// workgroup; the band loop kernel runs an image's general-path bands through
-// it one after another).  Every barrier inside is reached by all threads;
+// One band of BAND output rows of image k (one per K2 workgroup; the
+// band-loop form of round 4 was deleted in round 6: slower at the driver's
+// launch sizes, equal at 400 steps).  Every barrier inside is reached by all threads;
 // the only thread-level return follows the last one.
-template <int MODE, bool FP16, bool GENERAL_ONLY = false, int LDS_BYTES = K2_LDS>
+template <int MODE, bool FP16>
 FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *lds) {
   lds_u16_t *s_lut = (lds_u16_t *)lds;  // 768 entries (FP16), channel-major
   const int t = threadIdx.x;
@@ -2508,8 +2509,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   // VALU sequence, twelve per workgroup); 3 takes the general path
   auto p2 = [](int x) { return x == 1 || x == 2 || x == 4; };
   const bool pow2 = p2(G.he[0]) && p2(G.ve[0]) && p2(G.he[1]) && p2(G.ve[1]) && p2(G.he[2]) && p2(G.ve[2]);
-  if (!GENERAL_ONLY && P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && pow2 &&
-      true) {
+  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && pow2) {
     const int lut_b = FP16 ? 1536 : 0;
     LinTap *rtab = (LinTap *)(lds + lut_b);
     int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
@@ -2536,7 +2536,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
     }
     const int rgb_off = need;
     need += nrows * rw * 4 + 4;  // + a dummy word for the colour pass's off-crop pixels
-    if (need <= LDS_BYTES) {
+    if (need <= K2_LDS) {
       K2_STOP_AT(1, a.out_stride != 77);  // diagnostics: the band's set-up (record, LUT, taps, tile bounds)
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
       if (t < oy1 - oy0) {  // weights stored as the walk's multiplier operands, c << 8 (see hrow)
@@ -2822,15 +2822,15 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   }
   const int roi_off = need;
   need += nrows * step;
-  const bool tiled = need <= LDS_BYTES;
-  const bool staged = tiled || lut_b + nrows * step <= LDS_BYTES;  // (tap tables fit: see tabs)
+  const bool tiled = need <= K2_LDS;
+  const bool staged = tiled || lut_b + nrows * step <= K2_LDS;  // (tap tables fit: see tabs)
   uint8_t *roi = lds + (tiled ? roi_off : lut_b);
   // Bands too wide for LDS stage their rows in the image's rgb slot at their
   // absolute crop-row position; rows shared with a neighbouring band are
   // written with identical bytes by both.
   uint8_t *groi = a.arena + I.rgb_off;
   uint8_t *dst = staged ? roi : groi + (uint64_t)r0 * step;
-  const bool tabs = tap_b > 0 && lut_b <= LDS_BYTES / 2;
+  const bool tabs = tap_b > 0 && lut_b <= K2_LDS / 2;
   if (tabs) {  // [0, out_w): columns, [out_w, out_w + rows): the band's rows
     for (int i = t; i < out_w + (oy1 - oy0); i += K2T) {
       if (P.kind == 2)
@@ -2904,7 +2904,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   // (resize.cpp VResizeLinearVec_32s8u).  Columns in the scalar tail
   // (>= vec_end) keep the per-pixel path.
   const int hoff = (((tiled ? roi_off : lut_b) + nrows * step) + 15) & ~15;
-  const bool sep = P.kind == 3 && staged && tabs && hoff + nrows * out_w * 8 <= LDS_BYTES;
+  const bool sep = P.kind == 3 && staged && tabs && hoff + nrows * out_w * 8 <= K2_LDS;
   uint2 *H = (uint2 *)(lds + hoff);
   __syncthreads();
   if (sep) {
@@ -2924,7 +2924,7 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   }
   LdsRoi lr{roi, r0, step};
   // resize_area_lds reads up to 5 bytes past the staged rows
-  const bool pad8 = (int)(roi - lds) + nrows * step + 8 <= LDS_BYTES;
+  const bool pad8 = (int)(roi - lds) + nrows * step + 8 <= K2_LDS;
   RoiSrc gr{groi, (uint64_t)step};
   auto px = [&](int dy, int dx, int v[3]) {
     if (ep.in_cut(dy, dx)) {
@@ -3006,387 +3006,6 @@ __global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2_WPE
   k2_band<MODE, FP16>(a, (int)blockIdx.y, (int)blockIdx.x, lds);
 }
 
-// ======================================================================= //
-// K2L: one workgroup per image, looping over its bands                     //
-// ======================================================================= //
-// The per-band K2 above pays its whole set-up in every one of an image's 14
-// workgroups (record broadcast, LUT, column taps, cutout columns, tile bounds:
-// ~60% of its instructions), and each workgroup waits for its
-// plane tiles before it can start.  Here a workgroup owns one image: the
-// per-image set-up runs once, and band b + 1's plane tiles travel from HBM
-// straight into LDS (global_load_lds, no registers) while band b's column
-// walk runs.  Per band: [wait for the tiles] barrier -> colour pass (tiles ->
-// RGBx rows) -> barrier -> issue band b + 1's tile loads -> walk (RGBx ->
-// output).  The walk reads only the RGBx rows, the LUT and its band's row
-// taps (double-buffered), so the next band's loads may land under it.
-// Same arithmetic, line for line, as k2_band's linear fast path; images that
-// do not qualify (not 4:2:0, not a linear resize, a band too big for LDS)
-// run k2_band's general path band after band.
-
-// Plane tile bounds of one band (all wave-uniform).
-struct K2Band {
-  int r0, r1, nrows;
-  int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
-  int need;
-};
-FFCV_DEV K2Band k2l_band_geom(const ImgInfo &I, const ResizePlan &P, int oy0, int oy1, int base) {
-  K2Band g;
-  band_rows(P, oy0, oy1, &g.r0, &g.r1);
-  g.nrows = g.r1 - g.r0 + 1;
-  int need = base;
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    if (c >= I.ncomp) {
-      g.ty0[c] = g.tx0[c] = g.trows[c] = g.tpitch[c] = g.toff[c] = 0;
-      continue;
-    }
-    const int he = I.he[c], ve = I.ve[c], hsh = he >> 1, vsh = ve >> 1;  // 1 / 2 -> 0 / 1
-    int y0 = ((I.ri + g.r0) >> vsh) - (ve == 2 ? 1 : 0), y1 = ((I.ri + g.r1) >> vsh) + (ve == 2 ? 1 : 0);
-    int x0 = (I.rj >> hsh) - (he == 2 ? 1 : 0), x1 = ((I.rj + I.rw - 1) >> hsh) + (he == 2 ? 1 : 0);
-    y0 = max(y0, 0);
-    x0 = max(x0, 0);
-    y1 = min(y1, I.ch[c] - 1);
-    x1 = min(x1, I.cw[c] - 1);
-    g.ty0[c] = y0;
-    g.tx0[c] = x0 & ~3;  // whole dwords of the plane row
-    g.trows[c] = y1 - y0 + 1;
-    g.tpitch[c] = ((x1 + 4) & ~3) - g.tx0[c];
-    g.toff[c] = need;
-    need += g.trows[c] * g.tpitch[c];
-  }
-  g.need = need;  // end of the tiles (the RGBx rows sit at the image's fixed rgb_off above them)
-  return g;
-}
-
-// LDS: the plane tiles (the only target of the loads into LDS) in a static
-// array of their own, so the compiler can tell them apart from the LUT and
-// RGBx rows the walk reads and does not wait for the loads in flight before
-// each of those reads; the LUT and RGBx rows in the dynamic area.
-#ifndef K2L_TILE
-#define K2L_TILE 8192  // a band's plane tiles (4:2:0: <= 8 KB; bigger bands take the general path)
-#endif
-#ifndef K2L_DYN
-#define K2L_DYN 18432  // [LUT 1.5 KB][RGBx rows <= 16.5 KB]; with the tiles 26 KB: 6 workgroups per CU
-#endif
-#ifndef K2L_WPE
-#define K2L_WPE 6  // (5 workgroups per CU at 31 KB measured 1% slower)
-#endif
-#ifndef K2L_BPW
-#define K2L_BPW 7  // bands per workgroup (an image's 14 bands of 224 rows in two workgroups)
-#endif
-
-// Workgroup barrier that orders LDS only: __syncthreads' workgroup fence also
-// waits for every outstanding global store (gfx9 counts loads and stores in
-// one vmcnt), which would hold each band's colour pass behind the previous
-// band's output stores.
-FFCV_DEV void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <bool FP16>
-__global__ void __launch_bounds__(K2T) __attribute__((amdgpu_waves_per_eu(K2L_WPE))) jpeg_rrc_loop_kernel(JpegArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ __attribute__((aligned(16))) uint32_t s_tile[K2L_TILE / 4];
-  lds_u16_t *s_lut = (lds_u16_t *)lds;  // channel-major (lut_at)
-  const int t = threadIdx.x;
-  const int k = blockIdx.y;
-  const int out_h = a.p.out_h, out_w = a.p.out_w;
-  const int nb = (out_h + BAND - 1) / BAND;
-  const int b0 = blockIdx.x * K2L_BPW, b1 = min(nb, b0 + K2L_BPW);  // this workgroup's bands
-  K2Rec R;
-  R.load(a.info + k, t);
-  constexpr int LU = (768 + K2T - 1) / K2T;
-  uint16_t lv[LU];
-  if (FP16) {
-#pragma unroll
-    for (int u = 0; u < LU; u++) lv[u] = u * K2T + t < 768 ? lut_src(a.p.lut, u * K2T + t) : (uint16_t)0;
-  }
-  const uint2 *ktaps = a.taps && out_w + out_h <= K2_TAPS ? a.taps + (uint64_t)k * K2_TAPS : nullptr;
-  uint4 ct_pre = make_uint4(0, 0, 0, 0);
-  if (ktaps && 2 * (t % K2_COLS) + 1 < out_w) ct_pre = *(const uint4 *)(ktaps + 2 * (t % K2_COLS));
-  const int cut_y0 = a.cut ? a.cut[2 * k] : 0, cut_x0 = a.cut ? a.cut[2 * k + 1] : 0;
-  const int flip0 = a.flips ? a.flips[k] : 0;
-  if (k == 0 && b0 == 0 && t == 0) {  // K1 is done: close its arena (see arena_before_k1)
-    const unsigned long long top = a.arena_top[0];
-    if (top) {
-      a.arena_top[1] = top;
-      a.arena_top[0] = 0;
-    }
-  }
-  const ImgInfo I = k2_head(R);
-  if (I.status == -1) return;  // raw sample (handled by the raw kernel)
-  char *ob = (char *)a.out + a.out_stride * k;
-  const int esz = FP16 ? 2 : 1;
-  if (I.status != FFCV_SAMPLE_OK) {  // zero-fill this workgroup's rows
-    const uint64_t row = (uint64_t)out_w * 3 * esz, n = row * (min(out_h, b1 * BAND) - b0 * BAND);
-    for (uint64_t i = t; i < n; i += K2T) ob[row * b0 * BAND + i] = 0;
-    return;
-  }
-  const ResizePlan P = I.plan;
-  const int ri = I.ri, rj = I.rj, rw = I.rw;
-  bool fast = P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && I.taps &&
-              I.ncomp == 3 && !I.color_rgb && I.he[0] == 1 && I.ve[0] == 1 && I.he[1] == 2 && I.ve[1] == 2 &&
-              I.he[2] == 2 && I.ve[2] == 2 && I.cw[1] > 2 && I.cw[2] > 2;
-  // LDS: band b + 1's tiles land in s_tile while band b's walk reads the
-  // RGBx rows (sized for the workgroup's tallest band + the colour pass's
-  // dummy word) in the dynamic area
-  int tiles_max = 0, rows_max = 0;
-  for (int b = b0; fast && b < b1; b++) {
-    const K2Band gb = k2l_band_geom(I, P, b * BAND, min(out_h, b * BAND + BAND), 0);
-    tiles_max = max(tiles_max, gb.need);
-    rows_max = max(rows_max, gb.nrows);
-  }
-  constexpr int rgb_off = 1536;
-  fast = fast && tiles_max <= K2L_TILE && rgb_off + rows_max * rw * 4 + 4 <= K2L_DYN;
-  if (!fast) {  // the general path, one band after another
-    for (int b = b0; b < b1; b++) {
-      k2_band<JM_RRC, FP16, false, K2L_DYN>(a, k, b, lds);
-      __syncthreads();
-    }
-    return;
-  }
-  if (FP16) {
-#pragma unroll
-    for (int u = 0; u < LU; u++)
-      if (u * K2T + t < 768) s_lut[u * K2T + t] = lv[u];
-  }
-  Epilogue ep;
-  ep.out_h = out_h;
-  ep.out_w = out_w;
-  ep.cut_size = a.cut ? a.p.cutout_size : 0;
-  ep.cut_y = cut_y0;
-  ep.cut_x = cut_x0;
-  ep.flip = flip0;
-  ep.cut_before_flip = a.p.cutout_fill[3];
-  ep.fill[0] = a.p.cutout_fill[0];
-  ep.fill[1] = a.p.cutout_fill[1];
-  ep.fill[2] = a.p.cutout_fill[2];
-  const uint8_t *plane[3];
-  int pstride[3];
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    plane[c] = a.arena + I.poff[c];
-    pstride[c] = I.stride[c];
-  }
-  // this thread's output column pair (walk) and its linear taps (K1's table,
-  // flip applied): see k2_band for the arithmetic
-  const int tx = t % K2_COLS, sub = t / K2_COLS;
-  const bool walker = tx < out_w / 2;
-  const int dx0 = 2 * tx;
-  const LinTap l0 = tap_unpack(make_uint2(ct_pre.x, ct_pre.y)), l1 = tap_unpack(make_uint2(ct_pre.z, ct_pre.w));
-  const int a0w = l0.border ? 2048 : l0.c0, b0w = l0.border ? 0 : l0.c1;
-  const int a1w = l1.border ? 2048 : l1.c0, b1w = l1.border ? 0 : l1.c1;
-  const uint32_t w0 = ((uint32_t)a0w << 4) | ((uint32_t)b0w << 20), w1 = ((uint32_t)a1w << 4) | ((uint32_t)b1w << 20);
-  const uint32_t so0 = 4u * (uint32_t)l0.s, so1 = 4u * (uint32_t)l1.s;  // byte offsets in a row
-  const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
-  const uint32_t lq = FP16 ? 2u + 2u * lut_base(s_lut) : 2u;  // (lut_q)
-  uint32_t qfill[3];  // the cutout fill as lut_q's result
-  for (int c = 0; c < 3; c++) qfill[c] = FP16 ? lut_base(s_lut) + 2u * ep.fill[c] : ep.fill[c];
-  constexpr int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
-  // the counted wait below sets vmcnt's low field only (gfx9: 4 bits; the
-  // bits above it are expcnt / lgkmcnt); tests/test_isa_guards.py checks on
-  // the built code object that the walk issues exactly one store per row
-  static_assert(half > 0 && half < 16, "vmcnt(half) must fit the 4-bit field");
-  // does this wave walk (hold a lane with an output column pair)?
-  const bool wave_walks = ((t & ~63) % K2_COLS) < out_w / 2;
-
-  // plane tiles of a band: HBM -> LDS directly (global_load_lds_dword; lane
-  // l of a wave writes dword l of the wave's 64-dword run), row of dword i
-  // by a float reciprocal as in k2_band
-  auto issue_tiles = [&](const K2Band &g) {
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-      const int wpr = max(g.tpitch[c] >> 2, 1), n = g.trows[c] * (g.tpitch[c] >> 2);
-      const float rwp = __builtin_amdgcn_rcpf((float)wpr);
-      const uint8_t *src = plane[c] + (uint64_t)g.ty0[c] * pstride[c] + g.tx0[c];
-      uint8_t *tl = (uint8_t *)s_tile + g.toff[c];
-      for (int i0 = 0; i0 < n; i0 += K2T) {
-        const int i = i0 + t;
-        if (i < n) {
-          const int rr = (int)(((float)i + 0.5f) * rwp), q = i - __mul24(rr, wpr);
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void *)(src + (uint64_t)rr * pstride[c] + 4 * q),
-              (__attribute__((address_space(3))) void *)(tl + 4 * (i0 + (t & ~63))), 4, 0, 0);
-        }
-      }
-    }
-  };
-  // row taps: K1's packed table through the scalar cache (the walk's rows
-  // are wave-uniform; scalar loads count in lgkmcnt, not in the vmcnt the
-  // tile loads and output stores share)
-  const __attribute__((address_space(4))) uint32_t *rtaps =
-      (const __attribute__((address_space(4))) uint32_t *)(ktaps + out_w);
-  K2Band g = k2l_band_geom(I, P, b0 * BAND, min(out_h, b0 * BAND + BAND), 0);
-  issue_tiles(g);
-  bool full_walk = false;  // the previous band's walk issued exactly `half` stores after this band's loads
-  for (int b = b0; b < b1; b++) {
-    const int oy0 = b * BAND, oy1 = min(out_h, oy0 + BAND);
-    // this wave's tile loads (issued before the previous band's walk) have
-    // landed; the walk's output stores, issued after them, may still be in
-    // flight (vmcnt counts in issue order)
-    if (FP16 && full_walk)
-      __builtin_amdgcn_s_waitcnt(0x0f70 | half);  // vmcnt(half)
-    else
-      __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    lds_barrier();
-    // ---- colour pass (4:2:0, jdsample.c h2v2_fancy_upsample + jdcolor.c):
-    // k2_band's loop, over this band's tiles
-    const int r0 = g.r0, r1 = g.r1, nrows = g.nrows;
-    uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
-    {
-      TPlane tp[3];
-#pragma unroll
-      for (int c = 0; c < 3; c++) tp[c] = TPlane{(const uint8_t *)s_tile + g.toff[c], g.ty0[c], g.tx0[c], g.tpitch[c]};
-      const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
-      const int R0 = Y0 >> 1, R1 = Y1 >> 1, C0 = X0 >> 1, C1 = X1 >> 1;
-      const int npairs = (C1 - C0 + 2) >> 1;
-      const int ps = min(npairs, K2T);
-      const float rp = __builtin_amdgcn_rcpf((float)ps);
-      const int ng = (int)(((float)K2T + 0.5f) * rp);
-      const int gg = (int)(((float)t + 0.5f) * rp);
-      if (gg < ng)
-        for (int pr = t - __mul24(gg, ps); pr < npairs; pr += ps) {
-          const int C = C0 + 2 * pr;
-          const int cw = I.cw[1], ch = I.ch[1];
-          const int xm = max(C - 1, 0) - tp[1].c0, x0 = C - tp[1].c0;
-          const int x1 = min(C + 1, cw - 1) - tp[1].c0, x2 = min(C + 2, min(C1 + 1, cw - 1)) - tp[1].c0;
-          const int X = 2 * C;
-          bool vx[4];
-          int lx[4];
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            vx[j] = X + j >= X0 && X + j <= X1;
-            lx[j] = min(max(X + j, X0), X1) - tp[0].c0;
-          }
-          uint32_t *dummy = rgbx + nrows * rw;
-          for (int Rr = R0 + gg; Rr <= R1; Rr += ng) {
-            const int ru = max(Rr - 1, 0), rd = min(Rr + 1, ch - 1);
-            int qb[2][8];
-#pragma unroll
-            for (int pl = 0; pl < 2; pl++) {
-              const uint8_t *bp = tp[1 + pl].p;
-              const int pitch = tp[1 + pl].pitch, ty = tp[1 + pl].r0;
-              const uint8_t *rm = bp + __mul24(Rr - ty, pitch), *ra = bp + __mul24(ru - ty, pitch),
-                            *rb = bp + __mul24(rd - ty, pitch);
-              const int mm = rm[xm], m0 = rm[x0], m1 = rm[x1], m2 = rm[x2];
-              const int Tm = 3 * mm + ra[xm], T0 = 3 * m0 + ra[x0], T1 = 3 * m1 + ra[x1], T2 = 3 * m2 + ra[x2];
-              const int Bm = 3 * mm + rb[xm], B0 = 3 * m0 + rb[x0], B1 = 3 * m1 + rb[x1], B2 = 3 * m2 + rb[x2];
-              qb[pl][0] = (3 * T0 + Tm + 8) >> 4;
-              qb[pl][1] = (3 * T0 + T1 + 7) >> 4;
-              qb[pl][2] = (3 * B0 + Bm + 8) >> 4;
-              qb[pl][3] = (3 * B0 + B1 + 7) >> 4;
-              qb[pl][4] = (3 * T1 + T0 + 8) >> 4;
-              qb[pl][5] = (3 * T1 + T2 + 7) >> 4;
-              qb[pl][6] = (3 * B1 + B0 + 8) >> 4;
-              qb[pl][7] = (3 * B1 + B2 + 7) >> 4;
-            }
-#pragma unroll
-            for (int dy = 0; dy < 2; dy++) {
-              const int Y = 2 * Rr + dy;
-              const bool vy = Y >= Y0 && Y <= Y1;
-              const uint8_t *ly = tp[0].p + __mul24(min(max(Y, Y0), Y1) - tp[0].r0, tp[0].pitch);
-              uint32_t *orow = rgbx + __mul24(Y - Y0, rw) - X0;
-#pragma unroll
-              for (int j = 0; j < 4; j++) {
-                const int u = (j >> 1) * 4 + dy * 2 + (j & 1);
-                int v[3];
-                ycc_rgb(ly[lx[j]], qb[0][u], qb[1][u], v);
-                uint32_t *d = vy && vx[j] ? orow + X + j : dummy;
-                *d = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
-              }
-            }
-          }
-        }
-    }
-    lds_barrier();  // RGBx rows complete; the tiles are dead
-    // ---- the next band's tiles and row taps, in flight under the walk
-    if (b + 1 < b1) {
-      g = k2l_band_geom(I, P, oy0 + BAND, min(out_h, oy0 + 2 * BAND), 0);
-      issue_tiles(g);  // (s_tile: the walk does not read it)
-    }
-    // ---- column walk (resize.cpp HResizeLinear -> VResizeLinearVec_32s8u)
-    // (a row group is two whole waves: its rows are wave-uniform)
-    const int ya = __builtin_amdgcn_readfirstlane(oy0 + sub * half);
-    const int yb = __builtin_amdgcn_readfirstlane(min(oy1, ya + half));
-    full_walk = wave_walks && yb - ya == half;  // one store per row (FP16): `half` stores after the loads
-    if (walker) {
-      auto hrow = [&](int r, uint32_t H[6]) {
-        const uint32_t *row = rgbx + __mul24(r - r0, rw);
-        // words s and s + 1 as one ds_read2 per column (a border tap's second
-        // word has weight 0: at the crop's right edge it is the next row's
-        // first word or, in the last row, the dummy word)
-        const uint32_t *e0 = (const uint32_t *)((const uint8_t *)row + so0), *e1 = (const uint32_t *)((const uint8_t *)row + so1);
-        const uint32_t p0 = e0[0], q0 = e0[1];
-        const uint32_t p1 = e1[0], q1 = e1[1];
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-          const uint32_t sel = (uint32_t)c | 0x0c00u | ((uint32_t)(4 + c) << 16) | 0x0c000000u;
-          H[c] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(q0, p0, sel)),
-                                        __builtin_bit_cast(u16x2_t, w0), 0u, false) & 0x7fff00u;
-          H[3 + c] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(q1, p1, sel)),
-                                            __builtin_bit_cast(u16x2_t, w1), 0u, false) & 0x7fff00u;
-        }
-      };
-      auto mulhi24 = [](uint32_t x, uint32_t y) -> uint32_t {
-        return (uint32_t)(((uint64_t)(x & 0xffffffu) * (y & 0xffffffu)) >> 32);
-      };
-      int ca = -1, cb = -1;
-      uint32_t HA[6], HB[6];
-      for (int dy = ya; dy < yb; dy++) {
-        const LinTap ly = tap_unpack(make_uint2(rtaps[2 * dy], rtaps[2 * dy + 1]));
-        const int ra = min(max(ly.s, 0), P.sh - 1), rb = min(max(ly.s + 1, 0), P.sh - 1);
-        if (ra != ca) {
-          if (ra == cb) {
-#pragma unroll
-            for (int i = 0; i < 6; i++) HA[i] = HB[i];
-          } else {
-            hrow(ra, HA);
-          }
-          ca = ra;
-        }
-        if (rb != cb) {
-          hrow(rb, HB);
-          cb = rb;
-        }
-        uint32_t o[6];
-        const uint32_t c0 = ((uint32_t)ly.c0 & 0xfffu) << 8, c1 = ((uint32_t)ly.c1 & 0xfffu) << 8;
-#pragma unroll
-        for (int i = 0; i < 6; i++) o[i] = lut_q<FP16>(mulhi24(HA[i], c0) + mulhi24(HB[i], c1), lq);
-        if ((cut0 || cut1) && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
-          if (cut0) {
-            o[0] = qfill[0];
-            o[1] = qfill[1];
-            o[2] = qfill[2];
-          }
-          if (cut1) {
-            o[3] = qfill[0];
-            o[4] = qfill[1];
-            o[5] = qfill[2];
-          }
-        }
-        const uint64_t p0 = (uint64_t)dy * out_w + dx0;
-        if (FP16) {
-          const uint32_t h0 = lut_ld(o[0], 0), h1 = lut_ld(o[1], 1), h2 = lut_ld(o[2], 2);
-          const uint32_t h3 = lut_ld(o[3], 0), h4 = lut_ld(o[4], 1), h5 = lut_ld(o[5], 2);
-          typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-          u32x3 w;
-          w.x = h0 | (h1 << 16);
-          w.y = h2 | (h3 << 16);
-          w.z = h4 | (h5 << 16);
-          __builtin_nontemporal_store(w, (u32x3 *)((uint16_t *)ob + p0 * 3));
-        } else {
-          uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);
-          o16[0] = (uint16_t)(o[0] | (o[1] << 8));
-          o16[1] = (uint16_t)(o[2] | (o[3] << 8));
-          o16[2] = (uint16_t)(o[4] | (o[5] << 8));
-        }
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------- ctx -----
 struct ffcv_jpeg_ctx {
   uint64_t *dbg;
@@ -3403,7 +3022,6 @@ struct ffcv_jpeg_ctx {
   uint8_t *gtab;
   uint32_t *k1_order;  // max_batch slots (k1_order_kernel); used when k1_sorted
   bool k1_sorted;
-  int k2_loop_min;  // RRC launches of at least this many images run K2 as jpeg_rrc_loop_kernel
   uint64_t gtab_slot;
   uint32_t *eidx;  // entropy index (caller-owned), or NULL
   uint64_t eidx_n;
@@ -3456,14 +3074,6 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   {
     const char *o = getenv("FFCV_K1_ORDER");  // size-grouped K1 workgroups (A/B knob: 0 turns it off)
     c->k1_sorted = !o || atoi(o) != 0;
-    // the band-loop K2 (jpeg_rrc_loop_kernel) only when FFCV_K2_LOOP=1 (A/B
-    // knob).  Round 4 ran it for launches of >= 8,192 images (+2.8% then at
-    // C3's 12,288-image launches, -9% at the driver's 2,048-4,096); since
-    // round 5 the per-band kernel is as fast at 12,288 too (3.10 M vs
-    // 3.09-3.10 M at 400 steps; 135 vs 165-168 ns per image alone, DESIGN.md
-    // s6), so every launch size runs the per-band kernel
-    const char *l = getenv("FFCV_K2_LOOP");
-    c->k2_loop_min = l && atoi(l) != 0 ? 0 : INT_MAX;
   }
   c->max_h = max_height;
   c->max_w = max_width;
@@ -3720,13 +3330,6 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[2], s));
   dim3 g2((p->out_h + BAND - 1) / BAND, batch);
   if (!(only & 4)) {
-  } else if (batch >= c->k2_loop_min) {
-    if (fp16)
-      hipLaunchKernelGGL((jpeg_rrc_loop_kernel<true>), dim3((g2.x + K2L_BPW - 1) / K2L_BPW, batch), dim3(K2T),
-                         K2L_DYN, s, a);
-    else
-      hipLaunchKernelGGL((jpeg_rrc_loop_kernel<false>), dim3((g2.x + K2L_BPW - 1) / K2L_BPW, batch), dim3(K2T),
-                         K2L_DYN, s, a);
   } else if (fp16)
     hipLaunchKernelGGL((jpeg_color_resize_kernel<JM_RRC, true>), g2, dim3(K2T), K2_LDS, s, a);
   else

@@ -49,6 +49,7 @@ FFCV_DEV void store_px(void *out, uint64_t idx, const int v[3], const uint16_t *
 }
 
 #define RRC_THREADS 256
+static_assert(RRC_THREADS == 256, "rrc_band's row staging and walk assume four waves per workgroup");
 #ifndef RRC_BAND
 #define RRC_BAND 16  // output rows per workgroup
 #endif
@@ -93,8 +94,7 @@ struct LdsSrc {
 #ifndef RRC_WPE
 #define RRC_WPE 5  // waves per SIMD the raw kernel is compiled for (5 workgroups per CU by LDS)
 #endif
-// LDS of one band (the per-band kernel's, and the band-loop kernel's for the
-// bands it hands to rrc_band)
+// LDS of one band
 template <bool FP16>
 struct RrcLds {
   uint16_t lut[FP16 ? 768 : 1];
@@ -152,7 +152,9 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     int tpg = 64;
     while (tpg < (out_w >> 2)) tpg <<= 1;
     const int qq = t & (tpg - 1);
-    if (itaps && qq < (out_w >> 2)) {
+    // (rrc_taps_kernel writes the table for linear plans only: an area or
+    // copy crop's table is left unwritten, so it is not read)
+    if (itaps && P.kind == 3 && qq < (out_w >> 2)) {
       tq0 = *(const uint4 *)(itaps + 4 * qq);
       tq1 = *(const uint4 *)(itaps + 4 * qq + 2);
     }
@@ -178,10 +180,10 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     typedef uint32_t sx4_t __attribute__((ext_vector_type(4)));
     sx4_t v[RRC_STAGE_ROWS][2] = {};
     for (int cg = 0; cg < nch; cg += 128)  // (one pass for rows up to 2 KB: crops up to 677 px wide)
-      for (int rb0 = wv; rb0 < nrows; rb0 += 4 * RRC_STAGE_ROWS) {
+      for (int rb0 = wv; rb0 < nrows; rb0 += (RRC_THREADS / 64) * RRC_STAGE_ROWS) {
 #pragma unroll
         for (int q = 0; q < RRC_STAGE_ROWS; q++) {
-          const int r = rb0 + 4 * q;
+          const int r = rb0 + (RRC_THREADS / 64) * q;
           const uint64_t ra = row0 + (uint64_t)r * src.step;
           // chunks holding bytes of this row (none past the dataset's end)
           const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
@@ -195,7 +197,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         }
 #pragma unroll
         for (int q = 0; q < RRC_STAGE_ROWS; q++) {
-          const int r = rb0 + 4 * q;
+          const int r = rb0 + (RRC_THREADS / 64) * q;
           const uint64_t ra = row0 + (uint64_t)r * src.step;
           const int lim = r < nrows ? (int)(((ra & 15) + 3 * (uint64_t)P.sw + 15) >> 4) - cg : 0;
           if (ln < lim) s_src[r * nch + cg + ln] = __builtin_bit_cast(uint4, v[q][0]);

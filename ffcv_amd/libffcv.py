@@ -445,10 +445,12 @@ class JpegDecoder:
                                             int(batch), _p(out), int(out_stride), _p(status)),
                'ffcv_jpeg_decode_batch')
 
-    def set_diag(self, only=7, k2flags=0):
-        """Diagnostics: kernels a launch runs (bit 0 K1, bit 2 K2) and K2
-        timing-only flags, fixed on this context (never read per launch)."""
-        _check(lib().ffcv_jpeg_set_diag(self.handle, int(only), int(k2flags)), 'ffcv_jpeg_set_diag')
+    def set_diag(self, only=7):
+        """Diagnostics: kernels a launch runs (bit 0 K1, bit 1 the IDCT
+        kernel, bit 2 K2), fixed on this context (never read per launch).  The
+        C entry point's third argument (the K2 timing-only flags of rounds
+        1-4) must be 0 and is always passed as 0 here."""
+        _check(lib().ffcv_jpeg_set_diag(self.handle, int(only), 0), 'ffcv_jpeg_set_diag')
 
     def arena_used(self, stream=None):
         """(bytes the last entropy launch allocated, arena capacity)."""

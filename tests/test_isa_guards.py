@@ -1,12 +1,12 @@
 """Code-generation guards on the built gfx950 code object (no GPU needed).
 
-jpeg_rrc_loop_kernel<true> (ffcv_jpeg.hip, K2L) waits for the next band's
-plane tiles, copied HBM -> LDS by global_load_lds, with a counted
-``s_waitcnt vmcnt(half)``: the walk issues exactly one 12-byte output store
-per row after those loads, and vmcnt retires in order, so once at most `half`
-operations are outstanding the tile loads have landed.  That holds only while
-the compiler keeps the store unconditional in the walk loop's latch (ADVICE
-r4).  This test reads the disassembly of the library the product loads."""
+The hot kernels are tuned to their register budgets (K1 at 4 waves per SIMD,
+K2 at 6, K1b and the raw kernel at theirs): a source change that makes the
+compiler spill vector registers to scratch memory costs 5-30% without any
+wrong pixel (the C5 staging arrays moved to scratch ran 2.28 M
+vs 2.95 M).  These tests read the disassembly of the library the product
+loads and fail on any scratch access in those kernels.  (Round 6: the
+band-loop K2 and its counted-vmcnt guard were deleted.)"""
 import os
 import re
 import shutil
@@ -17,7 +17,6 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = '/opt/rocm/lib/llvm/bin'
 LIB = os.path.join(ROOT, 'ffcv_amd', 'libffcv_hip.so')
-HALF = 8  # jpeg_rrc_loop_kernel: rows per row group (BAND 16 / 2 row groups)
 
 
 def _disassemble():
@@ -52,30 +51,21 @@ def _kernel(asm, mangled):
     return [l.split('//')[0].strip() for l in lines[st[0] + 1:en] if l.strip()]
 
 
-def test_k2_loop_walk_store_count_matches_vmcnt():
+HOT = ['_Z19jpeg_entropy_kernelILi0EEv8JpegArgs',            # K1 (RRC)
+       '_Z16jpeg_idct_kernel8JpegArgs',                        # K1b
+       '_Z24jpeg_color_resize_kernelILi0ELb1EEv8JpegArgs',     # K2, fp16 LUT
+       '_Z24jpeg_color_resize_kernelILi0ELb0EEv8JpegArgs',     # K2, u8
+       '_Z14rrc_raw_kernelILb0EEv']                            # C5 raw kernel (prefix)
+
+
+def test_hot_kernels_do_not_spill_to_scratch():
     asm = _disassemble()
-    body = _kernel(asm, '_Z20jpeg_rrc_loop_kernelILb1EEv8JpegArgs')
-    assert any(l == f's_waitcnt vmcnt({HALF})' for l in body), 'the counted tile wait is gone'
-    stores = [i for i, l in enumerate(body) if l.startswith('global_store_dwordx3') and l.endswith(' nt')]
-    lds = [j for j, l in enumerate(body) if l.startswith('global_load_lds')]
-    assert stores and lds
-    # the band walk's store: the first streaming store after the tile loads
-    # (the general path's k2_band walk, inlined too, has its own)
-    after = [i for i in stores if i > lds[-1]]
-    assert after, 'no walk store after the tile loads'
-    i = after[0]
-    # the store sits in the walk loop's latch block: the next control-flow
-    # instruction is the loop's conditional exit test, with no other memory
-    # operation or branch in between -- so every walk row issues exactly one
-    # vector-memory instruction after the band's tile loads
-    for l in body[i + 1:i + 12]:
-        op = l.split()[0]
-        if op.startswith('s_cbranch_scc'):
-            break
-        assert not op.startswith(('s_cbranch', 's_branch', 'global_', 'buffer_', 'flat_', 's_setpc')), l
-    else:
-        raise AssertionError('no loop-exit test right after the walk store')
-    # and no other vector-memory instruction (loads included) between the
-    # band's last tile load and the walk store
-    between = [l for l in body[lds[-1] + 1:i] if l.split()[0].startswith(('global_', 'buffer_', 'flat_'))]
-    assert not between, between
+    for m in HOT:
+        body = _kernel(asm, m)
+        bad = [l for l in body if l.split()[0].startswith('scratch_')]
+        assert not bad, f'{m}: {len(bad)} scratch accesses, e.g. {bad[:3]}'
+
+
+def test_band_loop_kernel_is_gone():
+    asm = _disassemble()
+    assert 'jpeg_rrc_loop_kernel' not in asm

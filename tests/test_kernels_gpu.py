@@ -411,17 +411,13 @@ def test_jpeg_coefficients_match_oracle(hip_lib, oracle):
         assert np.array_equal(o[k, :len(want)], want), f'sample {k}'
 
 
-@pytest.mark.parametrize('k2_loop', ['0', '1'])
 @pytest.mark.parametrize('out_hw', [(224, 224), (288, 300)])
-def test_jpeg_rrc_matches_oracle(hip_lib, oracle, out_hw, k2_loop, monkeypatch):
+def test_jpeg_rrc_matches_oracle(hip_lib, oracle, out_hw):
     """Fused JPEG RRC + Cutout + flip (+ fp16 LUT) against the oracle; 288 x
     300 has out_w + out_h past K2_TAPS, where K1 writes no tap table and K2
     must not read one (the prefetch read past the allocation).
-    Both colour / resize kernels: the per-band one and the band-loop one
-    (FFCV_K2_LOOP=1 selects it: an A/B knob since round 5), whose general
-    path serves the 4:2:2 / 4:4:4 / grey images and the area-resize crops of
-    this set."""
-    monkeypatch.setenv('FFCV_K2_LOOP', k2_loop)  # read when the context is made
+    K2's general path serves the 4:2:2 / 4:4:4 / grey images and the
+    area-resize crops of this set."""
     OH, OW = out_hw
     torch = _torch()
     from ffcv_amd import libffcv as L

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Alternating A/B of one environment knob of the library (read when a decoder
-# context is made, e.g. FFCV_K2_LOOP, FFCV_K1_ORDER) on the C3 bench:
+# context is made, e.g. FFCV_K1_ORDER) on the C3 bench:
 #   tools/ab_env.sh <tag> <VAR> "<values>" <reps> [bench args]
 TAG=$1; VAR=$2; VALS=$3; R=$4; shift 4
 ARGS="--no-cpu-baseline --no-later-epochs --no-c5 --parity-rows 512 $@"

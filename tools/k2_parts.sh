@@ -1,10 +1,10 @@
 #!/bin/bash
-# Per-band K2 (jpeg_color_resize_kernel, FFCV_K2_LOOP=0) instructions / time by
+# Per-band K2 (jpeg_color_resize_kernel) instructions / time by
 # phase: diagnostic stop builds -DK2_STOP=n (1 set-up, 2 + plane tiles,
 # 3 + colour pass; tools/build_variant.sh k2stopN -DK2_STOP=N):
 #   tools/k2_parts.sh <tag> "new k2stop1 k2stop2 k2stop3"
 TAG=$1; V=${2:-"new k2stop1 k2stop2 k2stop3"}
-export TMPDIR=/tmp FFCV_K2_LOOP=0
+export TMPDIR=/tmp
 # warm the box first (first import of torch, the /tmp sample cache) with
 # output going to a file: a profiled run that is silent for 3 minutes is killed
 timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 --no-host-check --no-cpu-baseline --parity-rows 0 --no-kernel-events --no-later-epochs --no-c5 > gpurun_out/${TAG}_warm.log 2>&1 || { tail -3 gpurun_out/${TAG}_warm.log; exit 1; }

@@ -98,6 +98,12 @@ static_assert(FB_AC <= 11, "FB_AC > 11 is not supported: a 12-bit build failed t
 #define ACS_Z 24        // zigzag positions of a block the write pass stages in LDS
 #endif
 #define ACS_BYTES (ACS_Z * 2)
+#ifndef K1_CF_CPOL
+// cache policy of K1's window-coefficient stores (zeroing, direct, flush):
+// 0 default; A/B builds: 2 = nt, 16 = sc1 (write-through, the line leaves
+// the XCD's L2: MI355X_MICROARCH.md, "stores of each flavour")
+#define K1_CF_CPOL 0
+#endif
 #ifndef BAND
 #define BAND 16  // K2 output rows per workgroup
 #endif
@@ -649,8 +655,8 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
     if (l2) acs16[p2] = (int16_t)v2;
     // (issuing these under exec masks instead measured 0.6-2% slower: K1's
     // refill would then wait for every pending store, see BufReader)
-    __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, a1 && !l1 ? o1 : BUF_OOR, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, a2 && !l2 ? o2 : BUF_OOR, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((short)v, crs, a1 && !l1 ? o1 : BUF_OOR, 0, K1_CF_CPOL);
+    __builtin_amdgcn_raw_buffer_store_b16((short)v2, crs, a2 && !l2 ? o2 : BUF_OOR, 0, K1_CF_CPOL);
     z += zadd;
     const bool bend = z >= 64;
     {  // a staged block that ends leaves as three 16-byte stores
@@ -668,7 +674,7 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
       const uint32_t fo = fl ? boff * 2 : BUF_OOR;
 #pragma unroll
       for (int q = 0; q < ACS_BYTES / 16; q++)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, c[q]), crs, fo + 16 * q, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, c[q]), crs, fo + 16 * q, 0, K1_CF_CPOL);
     }
     stg = stg || bend;
     // the next block: (blk + 1, nph, mx', my')
@@ -696,7 +702,7 @@ FFCV_DEV void write_range(JShared &S, const TB &T, const uint32_t *words, uint32
   if (stg && z > 0 && inwin) {  // stopped inside a staged block: its positions below z are this lane's
     for (int q = 0; q < ACS_Z; q++) {
       const int c = acs16[q];
-      if (q < z && c != 0) __builtin_amdgcn_raw_buffer_store_b16((short)c, crs, (boff + (uint32_t)q) * 2, 0, 0);
+      if (q < z && c != 0) __builtin_amdgcn_raw_buffer_store_b16((short)c, crs, (boff + (uint32_t)q) * 2, 0, K1_CF_CPOL);
     }
   }
 }
@@ -1331,12 +1337,15 @@ FFCV_DEV uint64_t eidx_hash(uint32_t w0, uint32_t w1, uint32_t w2, int t) {
 // stores and the IDCT's block reads reach them (zeroed at allocation, ~300 us
 // earlier, they had been written back and the stores missed).
 FFCV_DEV void zero_window_coefs(const JShared &S, int16_t *coef, int t) {
-  // (a global-address-space pointer: global_store, not flat_store, which
-  // would also count in lgkmcnt)
-  typedef __attribute__((address_space(1))) u32x4_t gu4_t;
-  gu4_t *cz = (gu4_t *)(uintptr_t)wave_uniform((uint4 *)coef);
+#ifdef K1_NOZERO
+  return;  // diagnostics (wrong pixels): the zeroing's share of K1's traffic and time
+#endif
+  // (buffer stores: no flat_store, which would also count in lgkmcnt)
+  const __amdgpu_buffer_rsrc_t zrs =
+      __builtin_amdgcn_make_buffer_rsrc(wave_uniform((void *)coef), 0, (int)wuni(S.cf_bytes), BUF_CFG);
   const uint32_t n = wuni((uint32_t)(S.nwin * 8));
-  for (uint32_t i = (uint32_t)t; i < n; i += JL) cz[i] = (u32x4_t){0u, 0u, 0u, 0u};
+  for (uint32_t i = (uint32_t)t; i < n; i += JL)
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){0u, 0u, 0u, 0u}, zrs, 16 * i, 0, K1_CF_CPOL);
   wsync_mem();
 }
 
@@ -1686,6 +1695,9 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     a.status[k] = FFCV_SAMPLE_OK;
     info->status = -1;  // K2 skips
   }
+#ifdef K1_STOP
+  if (have && t == 0) info->status = -1;  // diagnostics: K1b / K2 skip (K1 stops before writing the record)
+#endif
   // no reservation until alloc_scratch makes one: an image that fails before
   // it (draws, parse, raw) must not report the previous launch's region
   // (ffcv_jpeg_arena_regions)

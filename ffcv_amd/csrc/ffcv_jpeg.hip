@@ -953,7 +953,11 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
   ffcv_sample smp = smp_in;
   smp.width = wuni(smp_in.width);
   smp.height = wuni(smp_in.height);
+  // (p through readfirstlane: the compiler kept the walk's position in a
+  // 64-bit vector register pair and branched on it under exec masks, ~20
+  // VALU per byte read; uniform, the branch and the address are scalar)
   auto B = [&](uint32_t p) -> int {
+    p = wuni(p);
     int v;
     if (p < HDR_BYTES)
       v = S.hdr[p];
@@ -972,6 +976,7 @@ FFCV_DEV int parse_header(JShared &S, const uint8_t *src, uint32_t nbytes, const
   if (nbytes < 4 || B(0) != 0xFF || B(1) != 0xD8) return FFCV_SAMPLE_BAD_MARKER;
   uint32_t p = 2;
   while (!have_sos) {
+    p = wuni(p);
     if (p + 4 > nbytes || B(p) != 0xFF) return FFCV_SAMPLE_BAD_MARKER;
     while (p < nbytes && B(p) == 0xFF) p++;
     if (p >= nbytes) return FFCV_SAMPLE_BAD_MARKER;

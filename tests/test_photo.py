@@ -103,7 +103,7 @@ def test_photo_rrc_cutout_flip_fp16_matches_oracle(hip_lib, oracle, out_hw):
     no per-image tap table (out_w + out_h > K2_TAPS) and more area crops."""
     torch = _torch()
     from ffcv_amd import libffcv as L
-    from test_kernels_gpu import _draw, _oracle_post
+    from tests.test_kernels_gpu import _draw, _oracle_post
     blobs, shapes, _, cases = _photos()
     reps = 14
     d_buf, d_smp, idx = _dev_set(blobs, shapes, reps)

@@ -619,11 +619,17 @@ def test_jpeg_rrc_fused_matches_staged(hip_lib, oracle):
         assert np.array_equal(res[1][4][k], want[0]), k
 
 
-def test_jpeg_k1_order_is_output_neutral(hip_lib, oracle, monkeypatch):
+@pytest.mark.parametrize('first', [None, 3, 10 ** 6])
+def test_jpeg_k1_order_is_output_neutral(hip_lib, oracle, monkeypatch, first):
     """K1's size-grouped workgroup order (k1_order_kernel, FFCV_K1_ORDER, on
     by default) only changes which wave decodes which image: crops, cutout,
     flips, status and pixels equal those of the plain order, bit for bit,
-    across a batch of mixed sizes with an out-of-range id."""
+    across a batch of mixed sizes with an out-of-range id.  The order kernel
+    also builds the launch's table cache from the batch's first image
+    (round 6), which the plain order does not use: `first` makes that image
+    one with optimised Huffman tables (image 3 of _jpeg_set: most workgroups
+    then miss the cache and build their own) or an out-of-range id (no
+    cache)."""
     torch = _torch()
     from ffcv_amd import libffcv as L
     rng = np.random.default_rng(57)
@@ -635,6 +641,8 @@ def test_jpeg_k1_order_is_output_neutral(hip_lib, oracle, monkeypatch):
     d_buf, d_table = _upload(buf), _dev(table)
     ids = rng.integers(0, len(imgs), 75).astype(np.int64)
     ids[11] = 10 ** 6  # out of range
+    if first is not None:
+        ids[0] = first
     B = len(ids)
     d_ids = torch.from_numpy(ids).to('cuda:0')
     dp = L.DrawParams()

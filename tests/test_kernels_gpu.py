@@ -674,7 +674,8 @@ def test_jpeg_k1_order_is_output_neutral(hip_lib, oracle, monkeypatch, first):
     for n, a_, b_ in zip(['crops', 'cut', 'flips', 'out', 'status'], *res):
         assert np.array_equal(a_, b_), n
     st = res[1][4]
-    assert st[11] != 0 and (np.delete(st, 11) == 0).all()
+    bad = [0, 11] if first == 10 ** 6 else [11]  # the out-of-range ids
+    assert (st[bad] != 0).all() and (np.delete(st, bad) == 0).all()
 
 
 def test_jpeg_entropy_index(hip_lib, oracle):

@@ -165,7 +165,7 @@ struct ImgInfo {
 // identical to the workgroup's first valid image share ONE LDS copy -- the
 // usual case, every encoder of a dataset writes the same tables -- and any
 // other image builds its own copy in global scratch (L1/L2-resident).
-struct __attribute__((aligned(16))) JTables {
+struct JTables {
   uint32_t lim[NSLOT][17];  // left-justified end of length-l codes
   int32_t valoff[NSLOT][17];
   uint8_t vals[NSLOT][256];
@@ -235,25 +235,6 @@ struct JShared {
 struct K1Shared {
   JTables tab;
   JShared w[JW * IPW];
-};
-
-// Decode tables of the launch's first image, built once per RRC launch by
-// k1_order_kernel (round 6).  Every encoder of a dataset writes the same
-// Huffman tables, so a K1 workgroup whose first valid image has the same
-// table slots and DHT bytes copies these 19 KB into LDS instead of building
-// them (~2 k VALU per image of first-level LUT and pair entries); any other
-// workgroup builds as before.  The tables are a pure function of what is
-// compared: the slot layout (nslots, slot_tab, sinfo, acmask) and each
-// slot's DHT bytes (16 counts + values).
-struct TabCache {
-  int valid;
-  int nslots;
-  int slot_tab[NSLOT];
-  uint32_t sinfo[NSLOT];
-  uint32_t acmask;
-  int dht_len[NSLOT];
-  uint8_t dht[NSLOT][16 + 256];
-  JTables tab __attribute__((aligned(16)));
 };
 
 // zigzag index of each natural (row-major) coefficient position; the entropy
@@ -938,7 +919,6 @@ struct JpegArgs {
   // (the sample id comes from ids[k]).
   uint32_t *eidx;
   uint64_t eidx_n;
-  TabCache *tcache;  // the launch's table cache (RRC launches with k1_order_kernel), or null
 };
 
 // Diagnostic stamps: lane 0 records wall_clock64 at phase boundaries into
@@ -1659,50 +1639,6 @@ __global__ void __launch_bounds__(K1O_T) k1_order_kernel(JpegArgs a, uint32_t *o
     if (k < a.batch) order[atomicAdd(&cnt[bk[i]], 1u)] = (uint32_t)k;
   }
   for (int k = t + K1O_PER * K1O_T; k < a.batch; k += K1O_T) order[atomicAdd(&cnt[bucket_of(size_of(k))], 1u)] = (uint32_t)k;
-  if (!a.tcache) return;
-  // ---- the launch's table cache (TabCache): the first image's header,
-  // parsed by wave 0 as K1 parses it, then its tables built by all threads
-  __shared__ JShared TS;
-  __shared__ int s_ok;
-  TabCache *tc = a.tcache;
-  ffcv_sample smp = {};
-  if (a.table) {
-    const uint64_t id = a.ids[0];
-    if (id < a.n_table) smp = a.table[id];
-  } else {
-    smp = a.samples[0];
-  }
-  const uint8_t *src = wave_uniform(a.base + smp.offset);
-  const uint32_t nbytes = wuni((uint32_t)smp.size);
-  for (int i = t; i < HDR_BYTES; i += K1O_T) TS.hdr[i] = i < (int)nbytes ? gld_u8(src + i) : (uint8_t)0;
-  __syncthreads();
-  if (t < JL) {  // (the parse's window fields follow the full-image mode: only the table fields are used)
-    const int st = smp.mode == 0 && smp.size > 0 ? parse_header(TS, src, nbytes, smp, a, 0, JM_FULL) : -1;
-    if (t == 0) s_ok = st == FFCV_SAMPLE_OK;
-  }
-  __syncthreads();
-  if (!s_ok) {
-    if (t == 0) tc->valid = 0;
-    return;
-  }
-  auto HB = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)TS.hdr[p] : (int)gld_u8(src + p); };
-  build_tables<K1O_T>(tc->tab, TS, HB, t);
-  for (int q = 0; q < TS.nslots; q++) {
-    const uint32_t d = TS.dht_off[TS.slot_tab[q]];
-    int total = 0;
-    for (int l = 0; l < 16; l++) total += HB(d + l);
-    for (int i = t; i < 16 + total; i += K1O_T) tc->dht[q][i] = (uint8_t)HB(d + i);
-    if (t == 0) tc->dht_len[q] = 16 + total;
-  }
-  if (t == 0) {
-    tc->nslots = TS.nslots;
-    for (int q = 0; q < NSLOT; q++) {
-      tc->slot_tab[q] = q < TS.nslots ? TS.slot_tab[q] : -1;
-      tc->sinfo[q] = q < TS.nslots ? TS.sinfo[q] : 0u;
-    }
-    tc->acmask = TS.acmask;
-    tc->valid = !tc->tab.bad;
-  }
 }
 
 template <int MODE>
@@ -1851,35 +1787,11 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
       match = !seg_any(diff, sg);
     }
   }
-  if (ref >= 0) {  // (ref is the same in every wave: the branch and its barriers are workgroup-uniform)
+  if (ref >= 0) {
     const JShared &R = KS.w[ref];
     const uint8_t *rsrc = R.src;
     auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)gld_u8(rsrc + p); };
-    // the launch's table cache (TabCache): the same slot layout and DHT bytes
-    // give the same tables, so copy them instead of building
-    const TabCache *tc = a.tcache;
-    bool hit = tc && tc->valid && tc->nslots == R.nslots && tc->acmask == R.acmask;
-    for (int q = 0; hit && q < NSLOT; q++)
-      if (q < R.nslots && (tc->slot_tab[q] != R.slot_tab[q] || tc->sinfo[q] != R.sinfo[q])) hit = false;
-    int diff = 0;
-    if (hit) {
-      for (int q = 0; q < R.nslots; q++) {
-        const uint32_t d = R.dht_off[R.slot_tab[q]];
-        const int len = tc->dht_len[q];
-        for (int i = (int)threadIdx.x; i < len; i += JW * JT) diff |= HBR(d + i) != (int)tc->dht[q][i];
-      }
-    }
-    hit = hit && !__syncthreads_or(diff);
-    if (hit) {
-      constexpr int NQ = (int)(sizeof(JTables) / 16);
-      static_assert(sizeof(JTables) % 16 == 0, "JTables copies as 16-byte words");
-      const uint4 *g = (const uint4 *)&tc->tab;
-      uint4 *l = (uint4 *)&KS.tab;
-      for (int i = (int)threadIdx.x; i < NQ; i += JW * JT) l[i] = g[i];
-      __syncthreads();
-    } else {
-      build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
-    }
+    build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
   }
   // (no workgroup barrier below this point: each wave runs on its own)
   if (!live) return;
@@ -3127,8 +3039,6 @@ struct ffcv_jpeg_ctx {
   uint8_t *gtab;
   uint32_t *k1_order;  // max_batch slots (k1_order_kernel); used when k1_sorted
   bool k1_sorted;
-  TabCache *tcache;  // the last RRC launch's table cache (k1_order_kernel -> K1)
-  bool tcache_on;
   uint64_t gtab_slot;
   uint32_t *eidx;  // entropy index (caller-owned), or NULL
   uint64_t eidx_n;
@@ -3155,7 +3065,6 @@ static void free_ctx(ffcv_jpeg_ctx *c) {
   (void)hipFree(c->taps);
   (void)hipFree(c->gtab);
   (void)hipFree(c->k1_order);
-  (void)hipFree(c->tcache);
   delete c;
 }
 
@@ -3182,8 +3091,6 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
   {
     const char *o = getenv("FFCV_K1_ORDER");  // size-grouped K1 workgroups (A/B knob: 0 turns it off)
     c->k1_sorted = !o || atoi(o) != 0;
-    const char *tc = getenv("FFCV_K1_TABLE_CACHE");  // A/B knob: 0 builds the tables in every K1 workgroup
-    c->tcache_on = !tc || atoi(tc) != 0;
   }
   c->max_h = max_height;
   c->max_w = max_width;
@@ -3200,7 +3107,6 @@ int ffcv_jpeg_create_arena(ffcv_jpeg_ctx **out, int max_batch, uint32_t max_heig
       (e = hipMalloc(&c->taps, sizeof(uint2) * K2_TAPS * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->gtab, c->gtab_slot * max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->k1_order, sizeof(uint32_t) * max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->tcache, sizeof(TabCache))) != hipSuccess ||
       // the memset above runs on the null stream, which the caller's
       // non-blocking streams do not wait for: finish it here (a first launch
       // on another stream read a stale counter left in reused memory and
@@ -3424,7 +3330,6 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[0], s));
   if (only & 1) {
     if (c->k1_sorted && batch > JW * IPW) {
-      a.tcache = c->tcache_on ? c->tcache : nullptr;  // built by the order kernel, read by K1
       hipLaunchKernelGGL(k1_order_kernel, dim3(1), dim3(K1O_T), 0, s, a, c->k1_order);
       FFCV_LAUNCH_CHECK("k1_order_kernel");
       a.k1_order = c->k1_order;
@@ -3432,7 +3337,6 @@ static int launch_rrc(ffcv_jpeg_ctx *c, JpegArgs &a, hipStream_t s, const ffcv_r
     hipLaunchKernelGGL((jpeg_entropy_kernel<JM_RRC>), dim3((batch + JW * IPW - 1) / (JW * IPW)), dim3(JW * JT), K1_PAD,
                        s, a);
     a.k1_order = nullptr;
-    a.tcache = nullptr;
     FFCV_LAUNCH_CHECK("jpeg_entropy_kernel<RRC>");
   }
   if (ev) FFCV_HIP_CHECK(hipEventRecord(ev[1], s));

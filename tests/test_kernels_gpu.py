@@ -624,12 +624,10 @@ def test_jpeg_k1_order_is_output_neutral(hip_lib, oracle, monkeypatch, first):
     """K1's size-grouped workgroup order (k1_order_kernel, FFCV_K1_ORDER, on
     by default) only changes which wave decodes which image: crops, cutout,
     flips, status and pixels equal those of the plain order, bit for bit,
-    across a batch of mixed sizes with an out-of-range id.  The order kernel
-    also builds the launch's table cache from the batch's first image
-    (round 6), which the plain order does not use: `first` makes that image
-    one with optimised Huffman tables (image 3 of _jpeg_set: most workgroups
-    then miss the cache and build their own) or an out-of-range id (no
-    cache)."""
+    across a batch of mixed sizes with an out-of-range id.  `first` makes
+    the batch's first image one with optimised Huffman tables (image 3 of
+    _jpeg_set) or an out-of-range id, so the workgroup that holds it in
+    either order differs in its shared-table owner."""
     torch = _torch()
     from ffcv_amd import libffcv as L
     rng = np.random.default_rng(57)

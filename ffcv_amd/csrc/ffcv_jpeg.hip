@@ -2414,6 +2414,135 @@ FFCV_DEV uint32_t lut_ld(uint32_t q, int c) { return ((const lds_u16_t *)(uintpt
 #ifndef K2_WPE
 #define K2_WPE 6  // waves per SIMD K2 is compiled for (6 WGs per CU at K2_LDS)
 #endif
+#ifndef K2_AREA_FAST
+#define K2_AREA_FAST 1  // 0: area crops take the general per-pixel path (A/B builds)
+#endif
+
+// K2's area walk: ResizeArea_Invoker (resize.cpp, INTER_AREA with both scales
+// in [1, 2)) for output columns dx0, dx0 + 1 over this thread's row group, from
+// the band's packed RGB rows in LDS (crop column x at byte xoff3 + 3 x of LDS
+// row r - r0).  Same arithmetic and order as resize_area: per source row the
+// horizontal sums buf = S[lo] a0 + S[lo + 1] a1 + S[lo + 2] a2 (a fixed
+// 3-tap body: a destination index at a scale < 2 covers at most 3 source
+// indices, and a tap past hi has weight 0, so x + S * 0 == x for these
+// non-negative sums), then sum = beta(lo) buf(lo), sum += beta(r) buf(r).
+// Consecutive output rows share at most their boundary source row, so one
+// cached row of sums covers the reuse.  The two columns' values of a channel
+// form one float2 (v_pk_mul_f32 / v_pk_add_f32: each lane is an ordinary
+// IEEE multiply or add, contraction off).  A row group is two whole waves: the
+// row loops and the cache test are scalar.
+typedef float k2f2 __attribute__((ext_vector_type(2)));
+template <bool FP16>
+FFCV_DEV void k2_area_walk(const Epilogue &ep, const ResizePlan &P, const AreaTaps *atab, const uint8_t *rgb,
+                           int pitch3, int xoff3, int r0, int oy0, int oy1, int sub, int dx0, uint32_t lutb,
+                           char *ob) {
+  const int half = (BAND + K2T / K2_COLS - 1) / (K2T / K2_COLS);  // rows per row group
+  const int ya = __builtin_amdgcn_readfirstlane(oy0 + sub * half);
+  const int yb = __builtin_amdgcn_readfirstlane(min(oy1, ya + half));
+  const int out_w = ep.out_w;
+  uint32_t xa[2], sh[2];  // a column's first tap: aligned byte offset in the row, byte shift
+  k2f2 wk[3];             // tap k's weight for (dx0, dx0 + 1)
+  {
+    const AreaTaps t0 = area_taps(P.sw, P.scale_x, ep.src_x(dx0)), t1 = area_taps(P.sw, P.scale_x, ep.src_x(dx0 + 1));
+    const uint32_t o0 = (uint32_t)(xoff3 + 3 * t0.lo), o1 = (uint32_t)(xoff3 + 3 * t1.lo);
+    xa[0] = o0 & ~3u;
+    sh[0] = o0 & 3u;
+    xa[1] = o1 & ~3u;
+    sh[1] = o1 & 3u;
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      wk[k] = (k2f2){t0.lo + k <= t0.hi ? t0.w(t0.lo + k) : 0.f, t1.lo + k <= t1.hi ? t1.w(t1.lo + k) : 0.f};
+  }
+  // a column's three tap pixels are 9 consecutive bytes: three aligned dword
+  // reads and v_alignbyte (misaligned LDS reads are several times slower)
+  auto hsum = [&](int r, k2f2 B[3]) {
+    const uint8_t *row = rgb + __mul24(r - r0, pitch3);
+    uint32_t e[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t *qa = (const uint32_t *)(row + xa[j]);
+      const uint32_t d0 = qa[0], d1 = qa[1], d2 = qa[2];
+      e[j][0] = __builtin_amdgcn_alignbyte(d1, d0, sh[j]);
+      e[j][1] = __builtin_amdgcn_alignbyte(d2, d1, sh[j]);
+      e[j][2] = d2 >> (8 * sh[j]);
+    }
+    auto bx = [&](int i) {
+      return (k2f2){(float)((e[0][i >> 2] >> (8 * (i & 3))) & 0xffu), (float)((e[1][i >> 2] >> (8 * (i & 3))) & 0xffu)};
+    };
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      k2f2 b = bx(c) * wk[0];  // (0 + x == x for x >= 0: the reference's zeroed buf)
+      b = b + bx(3 + c) * wk[1];
+      b = b + bx(6 + c) * wk[2];
+      B[c] = b;
+    }
+  };
+  const bool cut0 = ep.in_cut(ep.cut_y, dx0), cut1 = ep.in_cut(ep.cut_y, dx0 + 1);
+  int cr = -1;
+  k2f2 Hc[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) Hc[c] = (k2f2){0.f, 0.f};
+  for (int dy = ya; dy < yb; dy++) {
+    const AreaTaps ty = atab[dy - oy0];
+    k2f2 S[3];
+    for (int r = ty.lo; r <= ty.hi; r++) {
+      k2f2 H[3];
+      if (r == cr) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) H[c] = Hc[c];
+      } else {
+        hsum(r, H);
+      }
+      const k2f2 w = (k2f2){ty.w(r), ty.w(r)};
+      if (r == ty.lo) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) S[c] = w * H[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 3; c++) S[c] = S[c] + w * H[c];
+      }
+      if (r == ty.hi) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) Hc[c] = H[c];
+        cr = r;
+      }
+    }
+    uint32_t o[6];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      o[c] = (uint32_t)sat_u8i(ffcv_f2i_rn(S[c].x));
+      o[3 + c] = (uint32_t)sat_u8i(ffcv_f2i_rn(S[c].y));
+    }
+    if ((cut0 || cut1) && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
+      if (cut0) {
+        o[0] = ep.fill[0];
+        o[1] = ep.fill[1];
+        o[2] = ep.fill[2];
+      }
+      if (cut1) {
+        o[3] = ep.fill[0];
+        o[4] = ep.fill[1];
+        o[5] = ep.fill[2];
+      }
+    }
+    const uint64_t p0 = (uint64_t)dy * out_w + dx0;
+    if (FP16) {  // LUT entry (v, c) at lutb + 2 v + 512 c (lut_ld)
+      const uint32_t h0 = lut_ld(lutb + 2u * o[0], 0), h1 = lut_ld(lutb + 2u * o[1], 1), h2 = lut_ld(lutb + 2u * o[2], 2);
+      const uint32_t h3 = lut_ld(lutb + 2u * o[3], 0), h4 = lut_ld(lutb + 2u * o[4], 1), h5 = lut_ld(lutb + 2u * o[5], 2);
+      typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+      u32x3 w;
+      w.x = h0 | (h1 << 16);
+      w.y = h2 | (h3 << 16);
+      w.z = h4 | (h5 << 16);
+      __builtin_nontemporal_store(w, (u32x3 *)((uint16_t *)ob + p0 * 3));
+    } else {
+      uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);
+      o16[0] = (uint16_t)(o[0] | (o[1] << 8));
+      o16[1] = (uint16_t)(o[2] | (o[3] << 8));
+      o16[2] = (uint16_t)(o[4] | (o[5] << 8));
+    }
+  }
+}
 // One band of BAND output rows of image k (one per K2 workgroup; the
 // band-loop form of round 4 was deleted in round 6: slower at the driver's
 // launch sizes, equal at 400 steps).  Every barrier inside is reached by all threads;
@@ -2526,11 +2655,24 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
   // VALU sequence, twelve per workgroup); 3 takes the general path
   auto p2 = [](int x) { return x == 1 || x == 2 || x == 4; };
   const bool pow2 = p2(G.he[0]) && p2(G.ve[0]) && p2(G.he[1]) && p2(G.ve[1]) && p2(G.he[2]) && p2(G.ve[2]);
-  if (P.kind == 3 && P.vec_end == 3 * out_w && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && pow2) {
+  // area fast path (round 6): INTER_AREA crops with both scales in [1, 2)
+  // (every RRC crop larger than the output on both axes, up to 2x) of 4:2:0
+  // images: the same tiles and colour pass, the crop rows kept as packed RGB
+  // (3 bytes per pixel: 4-byte words would not fit a band's ~20 rows of up to
+  // 256 px), then a column-pair walk with one cached row of horizontal sums
+  // (as rrc_raw_kernel's area walk).  These bands took the general per-pixel
+  // path before, ~3x the time of a linear band (r5z2_c3_k2_by_crop_perband.log).
+  // (scale_x = 1 / (dw / sw) < 2 exactly when sw < 2 dw: integer tests keep
+  // the f64 scales out of this condition, which cost 11 VGPRs)
+  const bool area_fast = K2_AREA_FAST && P.kind == 2 && P.sw < 2 * P.dw && P.sh < 2 * P.dh && ncomp == 3 &&
+                         !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
+                         G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2;
+  if (((P.kind == 3 && P.vec_end == 3 * out_w) || area_fast) && (out_w & 1) == 0 && out_w <= 2 * K2_COLS && pow2) {
     const int lut_b = FP16 ? 1536 : 0;
     LinTap *rtab = (LinTap *)(lds + lut_b);
+    AreaTaps *atab = (AreaTaps *)(lds + lut_b);
     int ty0[3], tx0[3], trows[3], tpitch[3], toff[3];
-    int need = lut_b + (int)sizeof(LinTap) * BAND;
+    int need = lut_b + (area_fast ? (int)sizeof(AreaTaps) : (int)sizeof(LinTap)) * BAND;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
       if (c >= ncomp) {
@@ -2552,11 +2694,15 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       need += trows[c] * tpitch[c];
     }
     const int rgb_off = need;
-    need += nrows * rw * 4 + 4;  // + a dummy word for the colour pass's off-crop pixels
+    // area: RGB rows from luma column Xb = 2 * (rj >> 1) (the colour pass's
+    // first quad column), 12 bytes per chroma column pair, 4-byte aligned;
+    // + 16 bytes for the walk's aligned reads past the last row's end
+    const int pitch3 = 12 * (((((rj + rw - 1) >> 1) - (rj >> 1)) + 2) >> 1);
+    need += area_fast ? nrows * pitch3 + 16 : nrows * rw * 4 + 4;  // linear: + a dummy word for off-crop pixels
     if (need <= K2_LDS) {
       K2_STOP_AT(1, a.out_stride != 77);  // diagnostics: the band's set-up (record, LUT, taps, tile bounds)
       uint32_t *rgbx = (uint32_t *)(lds + rgb_off);
-      if (t < oy1 - oy0) {  // weights stored as the walk's multiplier operands, c << 8 (see hrow)
+      if (!area_fast && t < oy1 - oy0) {  // weights stored as the walk's multiplier operands, c << 8 (see hrow)
         LinTap lt = taps ? tap_unpack(rt_pre) : lin_tap(P.scale_y, P.inv_y, P.sh, oy0 + t);
         lt.c0 = (lt.c0 & 0xfff) << 8;
         lt.c1 = (lt.c1 & 0xfff) << 8;
@@ -2597,11 +2743,14 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
         }
         tp[c] = TPlane{(const uint8_t *)tl, ty0[c], tx0[c], tpitch[c]};
       }
+      // (after the tiles: its f64 arithmetic would raise the register peak
+      // while the tile loads are in flight)
+      if (area_fast && t < oy1 - oy0) atab[t] = area_taps(P.sh, P.scale_y, oy0 + t);
       __syncthreads();
       K2_STOP_AT(2, a.out_stride != 77);  // diagnostics: + the plane tiles
       const int Y0 = ri + r0, Y1 = ri + r1, X0 = rj, X1 = rj + rw - 1;
       if (ncomp == 3 && !G.color_rgb && G.he[0] == 1 && G.ve[0] == 1 && G.he[1] == 2 && G.ve[1] == 2 &&
-          G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {
+          G.he[2] == 2 && G.ve[2] == 2 && G.cw[1] > 2 && G.cw[2] > 2) {  // (every area_fast band)
         // 4:2:0 (jdsample.c h2v2_fancy_upsample, as upsample_quad_h2v2): each
         // thread owns a pair of adjacent chroma columns (C, C + 1) and walks
         // every ng-th chroma row of the band.  Column clamps, edge terms and
@@ -2657,6 +2806,28 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
               qb[pl][6] = (3 * B1 + B0 + 8) >> 4;
               qb[pl][7] = (3 * B1 + B2 + 7) >> 4;
             }
+            if (area_fast) {  // four packed RGB pixels per row: 3 words at byte 12 * pr of the row
+#pragma unroll
+              for (int dy = 0; dy < 2; dy++) {
+                const int Y = 2 * R + dy;
+                const uint8_t *ly = tp[0].p + __mul24(min(max(Y, Y0), Y1) - tp[0].r0, tp[0].pitch);
+                uint32_t px[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                  const int u = (j >> 1) * 4 + dy * 2 + (j & 1);
+                  int v[3];
+                  ycc_rgb(ly[lx[j]], qb[0][u], qb[1][u], v);
+                  px[j] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16);
+                }
+                if (Y >= Y0 && Y <= Y1) {
+                  uint32_t *d = rgbx + __mul24(Y - Y0, pitch3 >> 2) + 3 * pr;
+                  d[0] = px[0] | (px[1] << 24);
+                  d[1] = (px[1] >> 8) | (px[2] << 16);
+                  d[2] = (px[2] >> 16) | (px[3] << 8);
+                }
+              }
+              continue;
+            }
 #pragma unroll
             for (int dy = 0; dy < 2; dy++) {
               const int Y = 2 * R + dy;
@@ -2687,6 +2858,11 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       const int tx = t % K2_COLS, sub = t / K2_COLS;
       if (tx >= out_w / 2) return;
       const int dx0 = 2 * tx;
+      if (area_fast) {
+        k2_area_walk<FP16>(ep, P, atab, (const uint8_t *)rgbx, pitch3, 3 * (rj - 2 * (rj >> 1)), r0, oy0, oy1, sub,
+                           dx0, lut_base(s_lut), ob);
+        return;
+      }
       LinTap l0, l1;
       if (taps) {  // K1's table (flip applied): both columns in one 16-byte load (at the top)
         const uint4 q = ct_pre;

@@ -529,6 +529,59 @@ def test_jpeg_rrc_corner_upscale_fp16_cutout(hip_lib, oracle):
     assert bad.size == 0, f'samples {bad} differ'
 
 
+@pytest.mark.parametrize('out_hw', [(224, 224), (160, 192)])
+def test_jpeg_rrc_area_walk(hip_lib, oracle, out_hw):
+    """K2's area walk (round 6: INTER_AREA crops of 4:2:0 images with both
+    scales in [1, 2), packed RGB rows in LDS) against the oracle, u8 and fp16
+    with cutout and both flips: odd crop offsets (the rows start one pixel
+    before the crop), crops at the right / bottom edges, scales just above 1
+    and just below 2, exactly 2 (the general path), a band too wide for LDS
+    (the general path), and random draws at scale (0.85, 1)."""
+    OH, OW = out_hw
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    rng = np.random.default_rng(313)
+    shapes = [(256, 256), (256, 256), (255, 301), (300, 257), (460, 460), (460, 460), (256, 200), (240, 320)]
+    crops = [[0, 0, 256, 256], [3, 5, 230, 250], [25, 44, 230, 257], [44, 0, 256, 257],
+             [0, 0, 2 * OH - 1, 2 * OW - 1], [1, 1, 2 * OH, 2 * OW], [0, 0, 256, 200], [10, 63, 230, 257]]
+    for _ in range(24):  # random draws at the scales that make area crops
+        h, w = imagenet_like_shape(rng, 256)
+        shapes.append((h, w))
+        crops.append(None)
+    imgs = [natural_image(rng, h, w) for h, w in shapes]
+    blobs = [encode_jpeg(im, 90, '4:2:0') for im in imgs]
+    B = len(imgs)
+    hs = [s[0] for s in shapes]
+    ws = [s[1] for s in shapes]
+    dc, cut, flips = _draw(hip_lib, np.arange(B, dtype=np.uint64) + 77, hs, ws, 5, 1, cutout=24, flip_p=0.5,
+                           out=out_hw, scale=(0.85, 1.0))
+    crops = np.array([dc[k] if c is None else c for k, c in enumerate(crops)], np.int32)
+    assert (crops[:, 2] > OH).sum() > B // 2  # mostly area crops
+    d_buf, d_smp = _jpeg_dev(blobs, imgs)
+    dec = L.JpegDecoder(B, max(hs), max(ws), max(len(b) for b in blobs))
+    u8 = oracle.rrc_batch([(b, h, w, 0) for b, h, w in zip(blobs, hs, ws)], crops, OH, OW)
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    d_lut = torch.from_numpy(lut.view(np.int16)).to('cuda:0')
+    for use_lut in (False, True):
+        p = L.RRCParams()
+        p.out_h, p.out_w = OH, OW
+        p.cutout_size = 24
+        for i, f in enumerate((9, 200, 77)):
+            p.cutout_fill[i] = f
+        if use_lut:
+            p.lut = d_lut.data_ptr()
+        out = torch.zeros((B, OH, OW, 3), dtype=torch.float16 if use_lut else torch.uint8, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        dec.rrc(d_buf, d_smp, B, torch.from_numpy(crops).to('cuda:0'), torch.from_numpy(cut).to('cuda:0'),
+                torch.from_numpy(flips).to('cuda:0'), p, out, status)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == 0).all()
+        want = _oracle_post(u8, flips, cut, 24, (9, 200, 77), lut if use_lut else None)
+        got = out.cpu().numpy()
+        bad = np.argwhere((got.view(np.uint8) != want.view(np.uint8)).reshape(B, -1).any(1)).ravel()
+        assert bad.size == 0, f'samples {bad[:8]} differ (lut {use_lut})'
+
+
 def test_jpeg_corrupt_and_unsupported(hip_lib, oracle):
     torch = _torch()
     from ffcv_amd import libffcv as L

@@ -89,8 +89,13 @@ struct LdsSrc {
 //   writes one contiguous run of the output row.
 //   Otherwise (area downscale, copy, widths not a multiple of 4): the
 //   per-pixel restatement, over the staged rows when they fit.
-// rrc_taps_kernel's table: entries per image (even: 16-byte quads stay aligned)
-#define RAW_TAPS(p) (((p).out_w + (p).out_h + 1) & ~1)
+// rrc_taps_kernel's table: entries per image (even: 16-byte quads stay
+// aligned): linear plans use out_w + out_h (columns, then rows), area plans at
+// scales < 2 two per column (a 16-byte record: first tap, three weights)
+#define RAW_TAPS(p) ((max((p).out_w + (p).out_h, 2 * (p).out_w) + 1) & ~1)
+// an area plan whose column records rrc_taps_kernel writes: both scales < 2
+// (scale_x = 1 / (dw / sw) < 2 exactly when sw < 2 dw)
+FFCV_HD bool area_walk_plan(const ResizePlan &P) { return P.kind == 2 && P.sw < 2 * P.dw && P.sh < 2 * P.dh; }
 #ifndef RRC_WPE
 #define RRC_WPE 5  // waves per SIMD the raw kernel is compiled for (5 workgroups per CU by LDS)
 #endif
@@ -152,8 +157,8 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
     int tpg = 64;
     while (tpg < (out_w >> 2)) tpg <<= 1;
     const int qq = t & (tpg - 1);
-    // (rrc_taps_kernel writes the table for linear plans only: an area or
-    // copy crop's table is left unwritten, so it is not read)
+    // (rrc_taps_kernel writes these entries for linear plans only: an area
+    // crop's table holds the area walk's column records, read there)
     if (itaps && P.kind == 3 && qq < (out_w >> 2)) {
       tq0 = *(const uint4 *)(itaps + 4 * qq);
       tq1 = *(const uint4 *)(itaps + 4 * qq + 2);
@@ -268,11 +273,7 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
       }
     };
     if (P.kind == 2) {  // ResizeArea_Invoker: column taps once per thread, row taps from LDS
-      AreaTaps tx[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) tx[j] = area_taps(P.sw, P.scale_x, ep.src_x(dx0 + j));
-      RRC_STOP_AT(4, p.cutout_fill[3] != 77);  // diagnostics: + the area walk's column taps
-      if (P.scale_x < 2.0 && P.scale_y < 2.0) {
+      if (area_walk_plan(P)) {
         // Scales in [1, 2): a destination index takes at most 3 consecutive
         // source indices, so a fixed 3-tap horizontal body with zero weights
         // past `hi` is exact (x + S * 0.f == x for the non-negative sums
@@ -286,12 +287,25 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         // whole waves): the loop bounds and the cache test are scalar.
         int xo[4];  // the first tap pixel's byte offset in a row
         float wx[4][3];
+        if (itaps) {  // rrc_taps_kernel's column records (flip applied): one 16-byte load per column
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          xo[j] = 3 * tx[j].lo;
+          for (int j = 0; j < 4; j++) {
+            const uint4 e = *(const uint4 *)(itaps + 2 * (dx0 + j));
+            xo[j] = 3 * (int)e.x;
+            wx[j][0] = ffcv_u2f_bits(e.y);
+            wx[j][1] = ffcv_u2f_bits(e.z);
+            wx[j][2] = ffcv_u2f_bits(e.w);
+          }
+        } else {
 #pragma unroll
-          for (int k = 0; k < 3; k++) wx[j][k] = tx[j].lo + k <= tx[j].hi ? tx[j].w(tx[j].lo + k) : 0.f;
+          for (int j = 0; j < 4; j++) {
+            const AreaTaps tx = area_taps(P.sw, P.scale_x, ep.src_x(dx0 + j));
+            xo[j] = 3 * tx.lo;
+#pragma unroll
+            for (int k = 0; k < 3; k++) wx[j][k] = tx.lo + k <= tx.hi ? tx.w(tx.lo + k) : 0.f;
+          }
         }
+        RRC_STOP_AT(4, p.cutout_fill[3] != 77);  // diagnostics: + the area walk's column taps
         // A column's three tap pixels lo, lo + 1, lo + 2 are 9 consecutive
         // bytes: three ALIGNED 4-byte LDS reads cover them at any alignment
         // and v_alignbyte shifts them into place (bytes at fixed positions,
@@ -360,6 +374,9 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
         }
         return;
       }
+      AreaTaps tx[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) tx[j] = area_taps(P.sw, P.scale_x, ep.src_x(dx0 + j));
       for (int dy = gy0; dy < gy1; dy++) {
         const AreaTaps ty = s_at[dy - oy0];
         int v[12];
@@ -552,6 +569,16 @@ __global__ void __launch_bounds__(256) rrc_taps_kernel(const int32_t *__restrict
   const int k = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
   const ResizePlan P = make_plan(crops[4 * k + 3], crops[4 * k + 2], p.out_w, p.out_h);
   if (i == 0) plans[k] = P;
+  if (area_walk_plan(P)) {  // column records of the area walk: {lo, w(lo), w(lo + 1), w(lo + 2)}, 0 past hi
+    if (i >= p.out_w) return;
+    const int flip = flips ? flips[k] : 0;
+    const AreaTaps a = area_taps(P.sw, P.scale_x, flip ? p.out_w - 1 - i : i);
+    uint32_t w[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) w[j] = ffcv_f2u_bits(a.lo + j <= a.hi ? a.w(a.lo + j) : 0.f);
+    *(uint4 *)(taps + (uint64_t)k * RAW_TAPS(p) + 2 * i) = make_uint4((uint32_t)a.lo, w[0], w[1], w[2]);
+    return;
+  }
   if (P.kind != 3 || i >= p.out_w + p.out_h) return;
   LinTap l;
   if (i < p.out_w) {

@@ -2507,11 +2507,16 @@ FFCV_DEV void k2_area_walk(const Epilogue &ep, const ResizePlan &P, const AreaTa
         cr = r;
       }
     }
+    // cvRound + saturate_cast<uchar> of sums in [0, 255.5) (bytes times
+    // weights summing to 1 up to a few float roundings): S + 1.5 * 2^23
+    // rounds half-to-even into the float's low byte, one packed add per
+    // column pair (the saturation never acts); only that byte is used
     uint32_t o[6];
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-      o[c] = (uint32_t)sat_u8i(ffcv_f2i_rn(S[c].x));
-      o[3 + c] = (uint32_t)sat_u8i(ffcv_f2i_rn(S[c].y));
+      const k2f2 m = S[c] + (k2f2){12582912.0f, 12582912.0f};
+      o[c] = ffcv_f2u_bits(m.x);
+      o[3 + c] = ffcv_f2u_bits(m.y);
     }
     if ((cut0 || cut1) && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
       if (cut0) {
@@ -2527,8 +2532,9 @@ FFCV_DEV void k2_area_walk(const Epilogue &ep, const ResizePlan &P, const AreaTa
     }
     const uint64_t p0 = (uint64_t)dy * out_w + dx0;
     if (FP16) {  // LUT entry (v, c) at lutb + 2 v + 512 c (lut_ld)
-      const uint32_t h0 = lut_ld(lutb + 2u * o[0], 0), h1 = lut_ld(lutb + 2u * o[1], 1), h2 = lut_ld(lutb + 2u * o[2], 2);
-      const uint32_t h3 = lut_ld(lutb + 2u * o[3], 0), h4 = lut_ld(lutb + 2u * o[4], 1), h5 = lut_ld(lutb + 2u * o[5], 2);
+      auto la = [&](uint32_t b) { return lutb + 2u * (b & 0xffu); };
+      const uint32_t h0 = lut_ld(la(o[0]), 0), h1 = lut_ld(la(o[1]), 1), h2 = lut_ld(la(o[2]), 2);
+      const uint32_t h3 = lut_ld(la(o[3]), 0), h4 = lut_ld(la(o[4]), 1), h5 = lut_ld(la(o[5]), 2);
       typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
       u32x3 w;
       w.x = h0 | (h1 << 16);
@@ -2536,10 +2542,10 @@ FFCV_DEV void k2_area_walk(const Epilogue &ep, const ResizePlan &P, const AreaTa
       w.z = h4 | (h5 << 16);
       __builtin_nontemporal_store(w, (u32x3 *)((uint16_t *)ob + p0 * 3));
     } else {
-      uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);
-      o16[0] = (uint16_t)(o[0] | (o[1] << 8));
-      o16[1] = (uint16_t)(o[2] | (o[3] << 8));
-      o16[2] = (uint16_t)(o[4] | (o[5] << 8));
+      uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);  // low bytes of two values: v_perm
+      o16[0] = (uint16_t)__builtin_amdgcn_perm(o[1], o[0], 0x0c0c0400u);
+      o16[1] = (uint16_t)__builtin_amdgcn_perm(o[3], o[2], 0x0c0c0400u);
+      o16[2] = (uint16_t)__builtin_amdgcn_perm(o[5], o[4], 0x0c0c0400u);
     }
   }
 }

@@ -96,6 +96,9 @@ struct LdsSrc {
 // an area plan whose column records rrc_taps_kernel writes: both scales < 2
 // (scale_x = 1 / (dw / sw) < 2 exactly when sw < 2 dw)
 FFCV_HD bool area_walk_plan(const ResizePlan &P) { return P.kind == 2 && P.sw < 2 * P.dw && P.sh < 2 * P.dh; }
+#ifndef RRC_AREA_MAGIC
+#define RRC_AREA_MAGIC 1  // 0: the area walk rounds by v_rndne + v_cvt + v_med3 (A/B builds)
+#endif
 #ifndef RRC_WPE
 #define RRC_WPE 5  // waves per SIMD the raw kernel is compiled for (5 workgroups per CU by LDS)
 #endif
@@ -367,10 +370,54 @@ FFCV_DEV void rrc_band(const uint8_t *__restrict__ base, const ffcv_sample *__re
               cr = r;
             }
           }
+#if RRC_AREA_MAGIC
+          // cvRound + saturate_cast<uchar>: the sums lie in [0, 255.5) (bytes
+          // times weights that sum to 1 up to a few float roundings), so
+          // S + 1.5 * 2^23 rounds S half-to-even into the float's low byte and
+          // the saturation never acts: one (packed) add per value instead of
+          // v_rndne + v_cvt + v_med3, and the u8 bytes packed by v_perm
+          uint32_t bz[12];
+#pragma unroll
+          for (int i = 0; i < 12; i++) bz[i] = ffcv_f2u_bits(S[i] + 12582912.0f);
+          if (cmask && dy >= ep.cut_y && dy < ep.cut_y + ep.cut_size) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if ((cmask >> j) & 1) {
+                bz[3 * j] = ep.fill[0];
+                bz[3 * j + 1] = ep.fill[1];
+                bz[3 * j + 2] = ep.fill[2];
+              }
+          }
+          const uint64_t px = (uint64_t)dy * out_w + dx0;
+          if (FP16) {
+            uint32_t h[12];
+#pragma unroll
+            for (int i = 0; i < 12; i++) h[i] = s_lut[(bz[i] & 0xffu) * 3 + i % 3];
+            uint2 *o64 = (uint2 *)((uint16_t *)o + px * 3);
+            o64[0] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+            o64[1] = make_uint2(h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+            o64[2] = make_uint2(h[8] | (h[9] << 16), h[10] | (h[11] << 16));
+          } else {
+            typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+            uint32_t wd[3];
+#pragma unroll
+            for (int d = 0; d < 3; d++) {  // low bytes of four values: [a, b, 0, 0], [c, d, 0, 0] -> [a, b, c, d]
+              const uint32_t lo = __builtin_amdgcn_perm(bz[4 * d + 1], bz[4 * d], 0x0c0c0400u);
+              const uint32_t hi = __builtin_amdgcn_perm(bz[4 * d + 3], bz[4 * d + 2], 0x0c0c0400u);
+              wd[d] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            }
+            u32x3 w;
+            w.x = wd[0];
+            w.y = wd[1];
+            w.z = wd[2];
+            __builtin_nontemporal_store(w, (u32x3 *)((uint8_t *)o + px * 3));
+          }
+#else
           int v[12];
 #pragma unroll
           for (int i = 0; i < 12; i++) v[i] = sat_u8i(ffcv_f2i_rn(S[i]));
           put(dy, v);
+#endif
         }
         return;
       }

@@ -2720,18 +2720,25 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
       // dword); row = i / wpr by a float reciprocal: exact while the +0.5
       // margin, 0.5 / (i + 0.5) relative, exceeds v_rcp_f32's 1 ulp plus the
       // product's rounding (i < 2^20; tiles here hold < 2^13 dwords)
+      // Round 6: (float)i + 0.5 as t's float plus a constant, and the dword's
+      // address as a 32-bit offset (24-bit multiply-add: tile offsets stay
+      // below 2^24) from the component's scalar base (the saddr form) instead
+      // of 64-bit address arithmetic per dword
       constexpr int SU = 4;
       uint32_t sv[3][SU];
+      const float ft = (float)t + 0.5f;
+      typedef const __attribute__((address_space(1))) uint8_t gu8_t;
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         const int wpr = max(tpitch[c] >> 2, 1), n = trows[c] * (tpitch[c] >> 2);
         const float rwp = __builtin_amdgcn_rcpf((float)wpr);  // (1 ulp: far inside the +0.5 margin)
-        const uint8_t *src = gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c];
+        gu8_t *src = (gu8_t *)(uintptr_t)(gp[c].p + (uint64_t)ty0[c] * gp[c].stride + tx0[c]);
+        const uint32_t st = (uint32_t)gp[c].stride;
 #pragma unroll
         for (int u = 0; u < SU; u++) {
           const int i = u * K2T + t;
-          const int rr = (int)(((float)i + 0.5f) * rwp), q = i - __mul24(rr, wpr);
-          sv[c][u] = i < n ? *(const uint32_t *)(src + (uint64_t)rr * gp[c].stride + 4 * q) : 0u;
+          const int rr = (int)((ft + (float)(u * K2T)) * rwp), q = i - __mul24(rr, wpr);
+          sv[c][u] = i < n ? *(const __attribute__((address_space(1))) uint32_t *)(src + (__umul24((uint32_t)rr, st) + 4u * (uint32_t)q)) : 0u;
         }
       }
 #pragma unroll

@@ -6,21 +6,25 @@
 // TJFLAG_FASTDCT) = ifast IDCT + fancy upsampling + fixed-point YCbCr->RGB)
 // into a temp buffer, then crops and resizes on the CPU.
 //
-// Two launches per batch:
+// Launches per batch (launch_rrc): k1_order_kernel (size-sorted image order),
+// then three kernels on the launch's stream:
 //
-// K1 jpeg_entropy_kernel -- ONE WAVE (64 lanes) per image, ~26 KB of LDS, so
-// six images decode concurrently per CU.  (A self-synchronising Huffman
-// decode costs about the same latency at 64 or 256 lanes per image -- the
-// latency is the resynchronisation distance -- but a third of the lane-steps
-// at 64, so the wave-per-image shape triples throughput.)
-//   P0  the first 2 KB of the file are staged in LDS; one lane walks the
-//       markers (SOF/DHT/DQT/DRI/SOS), validates geometry and tables, and
-//       hands out Huffman table slots and LUT space
+// K1 jpeg_entropy_kernel -- ONE WAVE (64 lanes) per image, four images per
+// 256-thread workgroup sharing one LDS table set (38.8 KB: 16 images per CU).
+// (A self-synchronising Huffman decode costs about the same latency at 64 or
+// 256 lanes per image -- the latency is the resynchronisation distance -- but
+// a third of the lane-steps at 64, so the wave-per-image shape triples
+// throughput.)
+//   P0  gather (table[ids[k]]) and the RRC / cutout / flip draws (wave 0 for
+//       the workgroup); the first 2 KB of the file staged in LDS; the whole
+//       wave walks the markers (SOF/DHT/DQT/DRI/SOS) on wave-uniform values,
+//       validates geometry and tables, and hands out Huffman table slots
 //   P1  Huffman decode tables (jdhuff.c jpeg_make_d_derived_tbl, with its
-//       checks): per slot an 11-bit (AC) or 9-bit (DC) first-level LUT whose
-//       entry gives code length, extra-bit count and coefficient advance, a
-//       5-bit second level for longer codes, canonical limits for the rest;
-//       ifast dequantisation multipliers (jddctmgr.c)
+//       checks): per slot an 11-bit (luma AC), 10-bit (chroma AC) or 8-bit
+//       (DC) first-level LUT with two-symbol pair entries, a 5-bit second
+//       level for longer codes, canonical limits for the rest; ifast
+//       dequantisation multipliers (jddctmgr.c); built once per workgroup when
+//       its images' tables agree, else per image in global scratch
 //   P2  de-stuffing (0xFF00 -> 0xFF) of the entropy-coded segment in stream
 //       order, one coalesced dword per lane per step with a wave scan of the
 //       kept-byte counts, into an L2-resident scratch stream (zero-padded:
@@ -33,20 +37,23 @@
 //       guess changed re-decodes only until it reaches a block start it
 //       recorded before (same bit position and MCU phase: from there its old
 //       trajectory is exact).  Lane 0 is exact, so round r fixes lanes 0..r
-//       at worst; rounds end when no guess changes.
+//       at worst; rounds end when no guess changes.  (The entropy index skips
+//       these rounds for a sample decoded before.)
 //   P4  wave scan of blocks-started -> each lane's first block index
-//   P5  second decode: DC differences of every block, quantised AC
-//       coefficients (zigzag order) of the blocks the crop window needs
-//   P6  per-component DC prediction as a wave prefix scan
-//   P7  de-zigzag + dequantise + ifast IDCT (jidctfst.c) of the window's
-//       blocks -> component planes in HBM scratch; geometry record for K2
+//   P5  write pass: DC differences summed per lane, quantised AC coefficients
+//       (zigzag order) of the blocks the crop window needs, into a zeroed
+//       window; K2's resize plan and linear tap table
+//
+// K1b jpeg_idct_kernel -- one workgroup per image: DC prediction from the
+//   per-lane sums, de-zigzag + dequantise + ifast IDCT (jidctfst.c) of the
+//   window's blocks -> component planes in scratch.
 //
 // K2 jpeg_color_resize_kernel -- one workgroup per band of 16 output rows:
-//   stages the band's source rows of the crop as RGB in LDS (jdsample.c
-//   fancy upsampling + jdcolor.c fixed-point YCbCr->RGB, once per source
-//   pixel), then computes the band's output pixels with the OpenCV 4.5.4
-//   INTER_AREA restatement + flip / cutout / LUT epilogue.  Thousands of
-//   workgroups per batch keep the CUs occupied for this latency-bound part.
+//   stages the band's plane tiles and then its source rows of the crop as RGB
+//   in LDS (jdsample.c fancy upsampling + jdcolor.c fixed-point YCbCr->RGB,
+//   once per source pixel), then computes the band's output pixels with the
+//   OpenCV 4.5.4 resize restatement (linear walk, area walk, or the general
+//   per-pixel path) + flip / cutout / LUT epilogue.
 //
 // Every integer step matches libjpeg-turbo bit for bit
 // (tests/test_kernels_gpu.py); float steps use -ffp-contract=off.

@@ -7,7 +7,7 @@ TAG=${1:-c5c}; LIB=${2:+--lib $2}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python3 -u bench.py --config c5 --unique 1024 --steps 2 --warmup 1 --no-cpu-baseline --no-later-epochs --parity-rows 0 > gpurun_out/${TAG}_warm.log 2>&1 || { tail -3 gpurun_out/${TAG}_warm.log; exit 1; }
-for b in 0.60,0.76 0.80,0.86 0.94,1.0; do
+for b in ${BANDS:-0.60,0.76 0.80,0.86 0.94,1.0}; do
   d=gpurun_out/${TAG}_$b
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS --output-format csv -d $d -o run -- python3 bench.py $LIB --config c5 --unique 1024 --steps 20 --warmup 5 --uniform-launches --inflight 1 --no-cpu-baseline --no-host-check --parity-rows 0 --no-kernel-events --no-later-epochs --draw-scale $b > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
   python3 - "$d" "$b" <<'PY'

@@ -239,31 +239,9 @@ struct JShared {
   };
 };
 
-// Pooled later sync rounds (round 6, K1_POOL): the workgroup's lanes share
-// the re-decode tasks of its four images' later rounds, so a round whose
-// tasks are sparse in every image runs as one wave's steps instead of one per
-// image.  Exchange per (image, lane): the exit state and the event/count
-// bookkeeping, packed into two words (pool_rounds); the task list of the round.
-#ifndef K1_POOL
-#ifdef K1_STOP
-#define K1_POOL 0  // stop builds return at phase ends, which a pooled round's barriers cannot follow
-#else
-#define K1_POOL 1
-#endif
-#endif
-struct PoolX {
-  uint32_t xa[JW][JL];  // exit state: pos | z << 22 | ph << 28
-  uint32_t xb[JW][JL];  // cnt | eb << 12 | nev << 24 | cb << 27
-  uint64_t mask[JW];    // lanes of image w that re-decode this round
-  uint8_t task[JW * JL];
-  int flag[JW];  // 0: no sync rounds, 1: poolable, 2: needs its own rounds
-};
 struct K1Shared {
   JTables tab;
   JShared w[JW * IPW];
-#if K1_POOL
-  PoolX x;
-#endif
 };
 
 // zigzag index of each natural (row-major) coefficient position; the entropy
@@ -1339,136 +1317,6 @@ FFCV_DEV void build_tables(TB &T, const JShared &R, const HBF &HB, int tid) {
   bar();
 }
 
-#if K1_POOL
-// pool_rounds: the later sync rounds of the workgroup's images, pooled.  Every
-// wave of the workgroup calls it exactly once (images without rounds, failed
-// or absent ones with part 0), so its barriers line up: one to agree on the
-// mode, then per round four (tasks published / task list built / inputs read
-// / results written).  part: 0 no tasks, 1 poolable (the workgroup's shared
-// tables, lane ranges short enough for the packed words), 2 needs its own
-// rounds -- any 2 (or no 1) makes every wave return false and run its rounds
-// itself, unpooled.  Worker thread i takes task i (image order): a round
-// whose tasks are sparse in every image then runs as one wave's steps.  The
-// re-decode is the unpooled loop's sync_range<true> on the task's image (its
-// phase records, events and stream), so every state, count and event is the
-// same as the unpooled rounds produce (bit-exact output either way).
-FFCV_DEV uint32_t pool_pa(const DecState &x) { return x.pos | ((uint32_t)x.z << 22) | ((uint32_t)x.ph << 28); }
-FFCV_DEV DecState pool_ua(uint32_t v) {
-  DecState x;
-  x.pos = v & 0x3fffffu;
-  x.z = (int)((v >> 22) & 63u);
-  x.ph = (int)(v >> 28);
-  return x;
-}
-FFCV_DEV uint32_t pool_pb(uint32_t cnt, int eb, int nev, int cb) {
-  return cnt | ((uint32_t)eb << 12) | ((uint32_t)nev << 24) | ((uint32_t)cb << 27);
-}
-// the lane split of entropy_passes: lanes used and bits per lane range
-FFCV_DEV void lane_split(uint32_t total_bits, uint32_t &nthr, uint32_t &cbits) {
-  nthr = (total_bits + 191) / 192;
-  nthr = max(1u, min(nthr, (uint32_t)JL));
-  cbits = (total_bits + nthr - 1) / nthr;
-}
-FFCV_DEV bool pool_rounds(K1Shared &KS, const JpegArgs &a, int wi, int t, int part, DecState &g, DecState &e,
-                          uint32_t &my_cnt, int &my_nev, int &my_cb, int &my_eb, bool active, int &rounds) {
-  PoolX &X = KS.x;
-  if (t == 0) X.flag[wi] = part;
-  __syncthreads();
-  bool any_own = false, any_pool = false;
-#pragma unroll
-  for (int w = 0; w < JW; w++) {
-    any_own |= X.flag[w] == 2;
-    any_pool |= X.flag[w] == 1;
-  }
-  if (any_own || !any_pool) return false;
-  for (;;) {
-    DecState ng;
-    bool changed = false;
-    if (part == 1) {
-      ng.pos = seg_prev(e.pos, t);
-      ng.z = (int)seg_prev((uint32_t)e.z, t);
-      ng.ph = (int)seg_prev((uint32_t)e.ph, t);
-      changed = active && t > 0 && (ng.pos != g.pos || ng.z != g.z || ng.ph != g.ph);
-      X.xa[wi][t] = pool_pa(e);
-      X.xb[wi][t] = pool_pb(my_cnt, my_eb, my_nev, my_cb);
-    }
-    const uint64_t own = __ballot(changed);
-    if (t == 0) X.mask[wi] = own;
-    __syncthreads();
-    uint32_t pre = 0, n = 0;
-#pragma unroll
-    for (int w = 0; w < JW; w++) {
-      const uint32_t c = (uint32_t)__popcll(X.mask[w]);
-      pre += w < wi ? c : 0u;
-      n += c;
-    }
-    if (n == 0) break;  // (uniform: every wave read the same masks)
-    rounds++;
-    if (changed)
-      X.task[pre + __builtin_amdgcn_mbcnt_hi((uint32_t)(own >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)own, 0u))] =
-          (uint8_t)((wi << 6) | t);
-    __syncthreads();
-    const int i = (int)threadIdx.x;
-    const bool work = i < (int)n;
-    int img = 0, lane = 1;
-    DecState st = {}, ox = {};
-    uint32_t xb = 0;
-    if (work) {
-      const uint32_t code = X.task[i];
-      img = (int)(code >> 6);
-      lane = (int)(code & 63u);  // >= 1: lane 0's start never changes
-      st = pool_ua(X.xa[img][lane - 1]);
-      ox = pool_ua(X.xa[img][lane]);
-      xb = X.xb[img][lane];
-    }
-    __syncthreads();  // every input read before any result is written
-    if (work) {
-      JShared &W = KS.w[img];
-      const uint32_t total_bits = W.dlen * 8;
-      uint32_t nthr, cbits;
-      lane_split(total_bits, nthr, cbits);
-      const uint32_t my_end = lane == (int)nthr - 1 ? total_bits : min(total_bits, (uint32_t)(lane + 1) * cbits);
-      uint32_t cnt = xb & 0xfffu;
-      int eb = (int)((xb >> 12) & 0xfffu), nev = (int)((xb >> 24) & 7u), cb = (int)((xb >> 27) & 1u);
-      DecState ne;
-      if (st.pos >= my_end) {
-        ne = st;
-        cnt = 0;
-        nev = 0;
-        eb = 0;
-      } else {
-        const uint32_t evq = ((uint32_t)W.nblocks / nthr + NEV) / NEV;
-        const int esh = evq <= 1 ? 0 : 32 - __clz((int)(evq - 1));
-        const uint32_t *words = (const uint32_t *)(a.arena + W.ds_off);
-        uint32_t it = 0;
-        ne = sync_range<true>(W, KS.tab, words, st, my_end, lane, cnt, nev, cb, eb, ox, esh, it);
-      }
-      X.xa[img][lane] = pool_pa(ne);
-      X.xb[img][lane] = pool_pb(cnt, eb, nev, cb);
-    }
-    __syncthreads();
-    if (changed) {
-      e = pool_ua(X.xa[wi][t]);
-      const uint32_t b = X.xb[wi][t];
-      my_cnt = b & 0xfffu;
-      my_eb = (int)((b >> 12) & 0xfffu);
-      my_nev = (int)((b >> 24) & 7u);
-      my_cb = (int)((b >> 27) & 1u);
-      g = ng;
-    }
-  }
-  return true;
-}
-// a wave with no sync rounds of its own (no image, a failed one, an entropy
-// index hit) takes part in the workgroup's pooled rounds as a worker
-FFCV_DEV void pool_idle(K1Shared &KS, const JpegArgs &a, int wi, int t) {
-  DecState g = {}, e = {};
-  uint32_t c = 0;
-  int n = 0, cb = 0, eb = 0, r = 0;
-  pool_rounds(KS, a, wi, t, 0, g, e, c, n, cb, eb, false, r);
-}
-#endif
-
 // P3-P5 with table set T (the workgroup's LDS copy or the image's global
 // copy; separate instantiations so each reads its own address space).
 // Entropy index record of one sample: EIDX_WORDS words per lane range t >= 1,
@@ -1514,9 +1362,8 @@ FFCV_DEV void zero_window_coefs(const JShared &S, int16_t *coef, int t) {
 }
 
 template <class TB>
-FFCV_DEV bool entropy_passes(K1Shared &KS, int wi, bool poolable, JShared &S, const TB &T, const JpegArgs &a, int k, int t,
-                             int sg, const uint32_t *words, uint32_t total_bits, int16_t *coef, int16_t *dcd,
-                             uint64_t sample_id, bool dc_diffs) {
+FFCV_DEV bool entropy_passes(JShared &S, const TB &T, const JpegArgs &a, int k, int t, int sg, const uint32_t *words,
+                             uint32_t total_bits, int16_t *coef, int16_t *dcd, uint64_t sample_id, bool dc_diffs) {
   int rs0 = 0, rs1 = 0, rs2 = 0;
   uint32_t start_blk = 0;  // first block this lane starts
   // each lane's DC offsets and start block for jpeg_idct_kernel (non-coefficient modes)
@@ -1533,9 +1380,6 @@ FFCV_DEV bool entropy_passes(K1Shared &KS, int wi, bool poolable, JShared &S, co
   nthr = max(1u, min(nthr, (uint32_t)JL));
   const uint32_t cbits = (total_bits + nthr - 1) / nthr;
   const bool active = t < (int)nthr;
-  // pooled rounds pack a lane's block count and grid base into 12 bits each
-  // (a block takes >= 3 bits) and its bit position into 22
-  poolable = poolable && cbits < 12000u;
   const uint32_t my_end = active ? (t == (int)nthr - 1 ? total_bits : min(total_bits, (t + 1) * cbits)) : 0;
   // ---------------------------------------------------- entropy index ----
   uint32_t *rec = nullptr;
@@ -1555,9 +1399,6 @@ FFCV_DEV bool entropy_passes(K1Shared &KS, int wi, bool poolable, JShared &S, co
       STAMP(4);
       STAMP(5);
       if (a.dbg && t == 0) a.dbg[(uint64_t)k * 16 + 12] = ~0ull;  // index hit: no sync rounds
-#if K1_POOL
-      pool_idle(KS, a, wi, t);
-#endif
       zero_window_coefs(S, coef, t);
       if (active) {
         DecState g;
@@ -1594,11 +1435,7 @@ FFCV_DEV bool entropy_passes(K1Shared &KS, int wi, bool poolable, JShared &S, co
   if (active) e = sync_range<false>(S, T, words, g, my_end, t, my_cnt, my_nev, my_cb, my_eb, g, esh, it_lane);
   if (a.dbg) it_wave += __reduce_max_sync(~0ull, it_lane);
   int rounds = 0;
-  bool pooled = false;
-#if K1_POOL
-  pooled = pool_rounds(KS, a, wi, t, poolable ? 1 : 2, g, e, my_cnt, my_nev, my_cb, my_eb, active, rounds);
-#endif
-  while (!pooled) {
+  for (;;) {
     DecState ng;
     ng.pos = seg_prev(e.pos, t);
     ng.z = (int)seg_prev((uint32_t)e.z, t);
@@ -1865,7 +1702,7 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     }
   }
   ImgInfo *info = a.info + k;
-  const bool live = have && wuni((uint32_t)smp.mode) == 0;  // (wave-uniform: pool_idle's barriers sit under it)
+  const bool live = have && smp.mode == 0;
   if (have && smp.mode != 0 && t == 0) {  // raw samples are handled by rrc_raw_kernel / gather
     a.status[k] = FFCV_SAMPLE_OK;
     info->status = -1;  // K2 skips
@@ -1963,19 +1800,10 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     auto HBR = [&](uint32_t p) -> int { return p < HDR_BYTES ? (int)R.hdr[p] : (int)gld_u8(rsrc + p); };
     build_tables<JW * JT>(KS.tab, R, HBR, (int)threadIdx.x);
   }
-  // (no workgroup barrier below this point except pool_rounds', which every
-  // wave reaches exactly once: pool_idle on each early return)
-  if (!live) {
-#if K1_POOL
-    pool_idle(KS, a, wi, t);
-#endif
-    return;
-  }
+  // (no workgroup barrier below this point: each wave runs on its own)
+  if (!live) return;
   if (S.status != FFCV_SAMPLE_OK) {
     fail();
-#if K1_POOL
-    pool_idle(KS, a, wi, t);
-#endif
     return;
   }
   auto HB = [&](uint32_t p) -> int {
@@ -2005,9 +1833,6 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
     if (t == 0) S.status = FFCV_SAMPLE_BAD_MARKER;
     wsync_lds();
     fail();
-#if K1_POOL
-    pool_idle(KS, a, wi, t);
-#endif
     return;
   }
   // the window coefficients were zeroed by alloc_scratch
@@ -2154,14 +1979,12 @@ __global__ void __launch_bounds__(JW * JT) __attribute__((amdgpu_waves_per_eu(K1
   // so the refill loads use the scalar-base + 32-bit offset form)
   const uint32_t *words = wave_uniform((const uint32_t *)gds);
   const uint32_t total_bits = dlen * 8;
-  if (t == 0) S.dlen = dlen;  // (read by the pooled rounds' workers after a workgroup barrier)
 
 
   int16_t *dcd = (int16_t *)(a.arena + (((uint64_t)wuni((uint32_t)(S.dc_off >> 32)) << 32) | wuni((uint32_t)S.dc_off)));
   const uint64_t sid = a.ids && a.eidx ? a.ids[k] : ~0ull;
-  const bool any_bad =
-      match ? entropy_passes(KS, wi, true, S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF)
-            : entropy_passes(KS, wi, false, S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF);
+  const bool any_bad = match ? entropy_passes(S, KS.tab, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF)
+                             : entropy_passes(S, *gt, a, k, t, sg, words, total_bits, coef, dcd, sid, MODE == JM_COEF);
   wsync_mem();
   K1_STOP_AT(5, !any_bad);  // diagnostics: K1 up to the write pass
 

@@ -227,9 +227,10 @@ int ffcv_rrc_raw_batch(void *stream, const uint8_t *base,
 
 /* The same with a caller-provided device workspace (16-byte aligned, at
  * least ffcv_rrc_raw_workspace_bytes(batch, out_h, out_w) bytes; NULL runs
- * ffcv_rrc_raw_batch): each image's resize plan and linear tap table are
- * computed once (one small kernel, one thread per tap) instead of in every
- * band workgroup of the image.  Output is identical.  The workspace is
+ * ffcv_rrc_raw_batch): each image's resize plan and its linear tap table
+ * (or, for INTER_AREA crops at scales < 2, its column records) are computed
+ * once (one small kernel, one thread per tap) instead of in every band
+ * workgroup of the image.  Output is identical.  The workspace is
  * overwritten by the launch and must not be shared by launches in flight
  * on different streams. */
 int ffcv_rrc_raw_batch_ws(void *stream, const uint8_t *base,

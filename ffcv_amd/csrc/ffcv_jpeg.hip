@@ -2421,6 +2421,9 @@ FFCV_DEV uint32_t lut_ld(uint32_t q, int c) { return ((const lds_u16_t *)(uintpt
 #ifndef K2_WPE
 #define K2_WPE 6  // waves per SIMD K2 is compiled for (6 WGs per CU at K2_LDS)
 #endif
+#ifndef K2_SADDR_STORE
+#define K2_SADDR_STORE 1  // 0: the linear walk's per-row 64-bit output address (A/B builds)
+#endif
 #ifndef K2_AREA_FAST
 #define K2_AREA_FAST 1  // 0: area crops take the general per-pixel path (A/B builds)
 #endif
@@ -2537,7 +2540,12 @@ FFCV_DEV void k2_area_walk(const Epilogue &ep, const ResizePlan &P, const AreaTa
         o[5] = ep.fill[2];
       }
     }
-    const uint64_t p0 = (uint64_t)dy * out_w + dx0;
+    // the row's address is wave-uniform: scalar base + this thread's offset
+    typedef __attribute__((address_space(1))) uint8_t gbyte_t;
+    const uint64_t rb64 = (uint64_t)(uintptr_t)ob + (uint64_t)(uint32_t)dy * (uint32_t)((FP16 ? 6 : 3) * out_w);
+    gbyte_t *orow = (gbyte_t *)(uintptr_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb64 >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rb64));
+    const uint32_t xoff = (uint32_t)((FP16 ? 6 : 3) * dx0);
     if (FP16) {  // LUT entry (v, c) at lutb + 2 v + 512 c (lut_ld)
       auto la = [&](uint32_t b) { return lutb + 2u * (b & 0xffu); };
       const uint32_t h0 = lut_ld(la(o[0]), 0), h1 = lut_ld(la(o[1]), 1), h2 = lut_ld(la(o[2]), 2);
@@ -2547,9 +2555,10 @@ FFCV_DEV void k2_area_walk(const Epilogue &ep, const ResizePlan &P, const AreaTa
       w.x = h0 | (h1 << 16);
       w.y = h2 | (h3 << 16);
       w.z = h4 | (h5 << 16);
-      __builtin_nontemporal_store(w, (u32x3 *)((uint16_t *)ob + p0 * 3));
+      __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x3 *)(orow + xoff));
     } else {
-      uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);  // low bytes of two values: v_perm
+      __attribute__((address_space(1))) uint16_t *o16 =
+          (__attribute__((address_space(1))) uint16_t *)(orow + xoff);  // low bytes of two values: v_perm
       o16[0] = (uint16_t)__builtin_amdgcn_perm(o[1], o[0], 0x0c0c0400u);
       o16[1] = (uint16_t)__builtin_amdgcn_perm(o[3], o[2], 0x0c0c0400u);
       o16[2] = (uint16_t)__builtin_amdgcn_perm(o[5], o[4], 0x0c0c0400u);
@@ -2979,7 +2988,18 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
             o[5] = qfill[2];
           }
         }
+#if K2_SADDR_STORE
+        // (round 6) the row's address is wave-uniform (dy is): scalar base +
+        // this thread's fixed 32-bit offset (the store's saddr form), no
+        // 64-bit address arithmetic per row
+        typedef __attribute__((address_space(1))) uint8_t gbyte_t;
+        const uint64_t rb64 = (uint64_t)(uintptr_t)ob + (uint64_t)(uint32_t)dy * (uint32_t)(3 * esz * out_w);
+        gbyte_t *orow = (gbyte_t *)(uintptr_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb64 >> 32)) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rb64));
+        const uint32_t xoff = (uint32_t)(3 * esz * dx0);
+#else
         const uint64_t p0 = (uint64_t)dy * out_w + dx0;
+#endif
         if (FP16) {
           const uint32_t h0 = lut_ld(o[0], 0), h1 = lut_ld(o[1], 1), h2 = lut_ld(o[2], 2);
           const uint32_t h3 = lut_ld(o[3], 0), h4 = lut_ld(o[4], 1), h5 = lut_ld(o[5], 2);
@@ -2989,9 +3009,17 @@ FFCV_DEV void k2_band(const JpegArgs &a, const int k, const int band, uint8_t *l
           w.y = h2 | (h3 << 16);
           w.z = h4 | (h5 << 16);
           // streaming output: non-temporal (measured +2.7% C3 over plain stores)
+#if K2_SADDR_STORE
+          __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x3 *)(orow + xoff));
+#else
           __builtin_nontemporal_store(w, (u32x3 *)((uint16_t *)ob + p0 * 3));
+#endif
         } else {
+#if K2_SADDR_STORE
+          __attribute__((address_space(1))) uint16_t *o16 = (__attribute__((address_space(1))) uint16_t *)(orow + xoff);
+#else
           uint16_t *o16 = (uint16_t *)((uint8_t *)ob + p0 * 3);
+#endif
           o16[0] = (uint16_t)(o[0] | (o[1] << 8));
           o16[1] = (uint16_t)(o[2] | (o[3] << 8));
           o16[2] = (uint16_t)(o[4] | (o[5] << 8));

@@ -213,6 +213,47 @@ def test_raw_rrc_area_walk(hip_lib, oracle):
             assert np.array_equal(got.view(np.uint16), want.view(np.uint16)), (out, cbf)
 
 
+def test_area_walk_extreme_values(hip_lib, oracle):
+    """The area walks (raw C5 and JPEG K2) round by adding 1.5 * 2^23 and keep
+    the low byte, which is exact only while every sum stays in [0, 255.5):
+    saturated (255 / 0) images and a 255 / 0 checkerboard at area scales just
+    above 1 and just below 2, u8 and fp16, against the oracle."""
+    torch = _torch()
+    from ffcv_amd import libffcv as L
+    h = w = 460
+    yy, xx = np.mgrid[:h, :w]
+    checker = np.where(((yy + xx) & 1)[..., None], 255, 0).astype(np.uint8).repeat(3, 2)
+    imgs = [np.full((h, w, 3), 255, np.uint8), np.zeros((h, w, 3), np.uint8), checker, checker]
+    crops = np.array([[0, 0, 449, 451], [3, 5, 447, 449], [0, 1, 450, 449], [1, 0, 447, 447]], np.int32)
+    lut = oracle.normalize_lut(np.array([0.485, 0.456, 0.406]) * 255, np.array([0.229, 0.224, 0.225]) * 255)
+    for out in ((448, 448), (224, 226)):
+        u8 = oracle.rrc_batch([(x.reshape(-1), h, w, 1) for x in imgs], crops, *out)
+        assert np.array_equal(_run_raw_rrc(hip_lib, imgs, crops, out), u8), out
+        got = _run_raw_rrc(hip_lib, imgs, crops, out, lut=lut)
+        assert np.array_equal(got.view(np.uint16), _oracle_post(u8, lut=lut).view(np.uint16)), out
+    # JPEG (K2's area walk): 4:2:0 encodings of the same extremes
+    jimgs = [np.full((256, 256, 3), 255, np.uint8), np.zeros((256, 256, 3), np.uint8), checker[:256, :256].copy()]
+    blobs = [encode_jpeg(im, 95, '4:2:0') for im in jimgs]
+    jcrops = np.array([[0, 0, 256, 256], [3, 1, 250, 253], [1, 2, 230, 240]], np.int32)
+    d_buf, d_smp = _jpeg_dev(blobs, jimgs)
+    B = len(jimgs)
+    dec = L.JpegDecoder(B, 256, 256, max(len(b) for b in blobs))
+    u8 = oracle.rrc_batch([(b, 256, 256, 0) for b in blobs], jcrops, 224, 224)
+    d_lut = torch.from_numpy(lut.view(np.int16)).to('cuda:0')
+    for use_lut in (False, True):
+        p = L.RRCParams()
+        p.out_h, p.out_w = 224, 224
+        if use_lut:
+            p.lut = d_lut.data_ptr()
+        o = torch.zeros((B, 224, 224, 3), dtype=torch.float16 if use_lut else torch.uint8, device='cuda:0')
+        status = torch.full((B,), -1, dtype=torch.int32, device='cuda:0')
+        dec.rrc(d_buf, d_smp, B, torch.from_numpy(jcrops).to('cuda:0'), None, None, p, o, status)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == 0).all()
+        want = _oracle_post(u8, lut=lut if use_lut else None)
+        assert np.array_equal(o.cpu().numpy().view(np.uint8), want.view(np.uint8)), use_lut
+
+
 def test_raw_rrc_448_c5(hip_lib, oracle):
     """C5 shapes through the LDS-staged bands: device draws over 512x512
     sources (linear and area crops), plus a full-frame area crop, odd-offset
